@@ -1,0 +1,152 @@
+/*
+ * mtq_amd.h — C ABI of the MI355X-native (gfx950 / CDNA4) fake-quantization and
+ * calibration kernels (libmtq_amd.so).
+ *
+ * This is the drop-in boundary for the hot path of ModelOpt's PTQ fake quantization
+ * (`modelopt.torch.quantization`).  Every entry point here replaces one function of the
+ * reference's native extension ABI (pybind modules modelopt_cuda_ext / _fp8 / _mx built by
+ * modelopt/torch/quantization/extensions.py:28-72) or one ATen reduction the reference's
+ * Python layer issues on the hot path.  Reference citations are relative to the reference
+ * repository root.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch types.  All tensors are dense, contiguous and
+ *     device-resident (HBM).  `x` and `y` may alias (in-place, as fake_tensor_quant_).
+ *   - Element dtype codes: MTQ_F32, MTQ_F16, MTQ_BF16, MTQ_F64.  All arithmetic is fp32
+ *     (the reference casts to float in every kernel and in its ATen fallback).
+ *   - `amax` pointers may be any of the dtype codes (`amax_dtype`), converted to fp32 on
+ *     load (reference: `amax.to(at::ScalarType::Float)`, tensor_quant_gpu.cu:84).
+ *   - Every launcher takes an explicit hipStream_t (reference kernels use
+ *     c10::cuda::getCurrentCUDAStream(), tensor_quant_gpu.cu:79).  Launchers never
+ *     synchronise, never allocate, and are safe to capture in a hipGraph.
+ *   - Return value: MTQ_OK (0) or a negative MTQ_ERR_* code; nothing throws across the ABI
+ *     (the reference raises TORCH_CHECK / std::invalid_argument, tensor_quant_mx.cu:337).
+ */
+#ifndef MTQ_AMD_H_
+#define MTQ_AMD_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- dtype / format / status codes -------------------------------------------------- */
+enum mtq_dtype { MTQ_F32 = 0, MTQ_F16 = 1, MTQ_BF16 = 2, MTQ_F64 = 3 };
+
+/* Element / scale formats.  Same order and names as the reference's `enum class Types`
+ * (modelopt/torch/kernels/quantization/gemm/tensor_quant_mx.h:38). */
+enum mtq_format {
+  MTQ_E4M3 = 0, MTQ_E5M2 = 1, MTQ_INT8 = 2, MTQ_E0M3 = 3, MTQ_E1M2 = 4,
+  MTQ_E3M0 = 5, MTQ_E2M1 = 6, MTQ_E3M2 = 7, MTQ_E2M3 = 8, MTQ_E8M0 = 9
+};
+
+enum mtq_status {
+  MTQ_OK = 0,
+  MTQ_ERR_INVALID_ARG = -1,
+  MTQ_ERR_DTYPE = -2,
+  MTQ_ERR_BLOCKSIZE = -3, /* reference: "Blocksize for fused call must be one of {8, 16, 32}" */
+  MTQ_ERR_FORMAT = -4,
+  MTQ_ERR_LAUNCH = -5,    /* hipGetLastError() after launch; see mtq_last_hip_error() */
+  MTQ_ERR_NO_DEVICE = -6
+};
+
+/* Human-readable message for a status code (static storage). */
+const char *mtq_status_string(int status);
+/* hipError_t of the most recent failing launch on this thread (0 if none). */
+int mtq_last_hip_error(void);
+/* Library version: major*10000 + minor*100 + patch. */
+int mtq_version(void);
+
+/* ---- INT-n fake quant ----------------------------------------------------------------
+ * y = clamp(rint(x * s), min_bound, max_bound) / s,  s = max_bound / amax (fp32),
+ * max_bound = 2^(num_bits-1+unsigned) - 1, min_bound = 0 | -max_bound | -max_bound-1
+ * (unsigned | narrow_range | full); amax <= 2^-24 quantizes to (signed) zero.
+ * Bit-exact with the reference's ATen path `_tensor_quant`
+ * (modelopt/torch/quantization/tensor_quant.py:607-645).
+ *
+ * mtq_fake_tensor_quant replaces `fake_tensor_quant` / `fake_tensor_quant_`
+ * (tensor_quant.cpp:39-56 -> tensor_quant_gpu.cu:59-98): per-tensor, amax has 1 element. */
+int mtq_fake_tensor_quant(const void *x, void *y, int64_t n, int dtype, const void *amax,
+                          int amax_dtype, int num_bits, int is_unsigned, int narrow_range,
+                          hipStream_t stream);
+
+/* Replaces `fake_tensor_quant_with_axis` (tensor_quant.cpp:58-64 ->
+ * tensor_quant_gpu.cu:100-140): channel of element i is (i / inner) % axis_size where
+ * inner = stride(axis) of the contiguous input; amax has axis_size elements.  Also the
+ * static block-quant path (input reshaped to (-1, block) with axis 0,
+ * tensor_quantizer.py:975-1061). */
+int mtq_fake_tensor_quant_with_axis(const void *x, void *y, int64_t n, int dtype,
+                                    const void *amax, int amax_dtype, int64_t axis_size,
+                                    int64_t inner, int num_bits, int is_unsigned,
+                                    int narrow_range, hipStream_t stream);
+
+/* ---- FP8 E4M3 fake quant ---------------------------------------------------------------
+ * safe = amax <= 2^-24 ? 1 : amax; s = RN(RN(1/safe) * 448) (Python `448.0 / t` is
+ * t.reciprocal() * 448); inv = 1/s;
+ * y = fp32(e4m3_rne(clamp(x*s, -448, 448))) * inv   (gfx950 v_cvt_pk_fp8_f32, OCP e4m3fn).
+ * Bit-exact with `_fp8_eager` (tensor_quant.py:46-59).
+ * Replaces `fake_e4m3fy` (tensor_quant_gpu_fp8.cu:90-107). */
+int mtq_fake_e4m3fy(const void *x, void *y, int64_t n, int dtype, const void *amax,
+                    int amax_dtype, hipStream_t stream);
+/* Replaces `fake_e4m3fy_with_axis` (tensor_quant_gpu_fp8.cu:66-88); also the FP8 static
+ * block path (amax [rows*K/block, 1] on the (-1, block) view). */
+int mtq_fake_e4m3fy_with_axis(const void *x, void *y, int64_t n, int dtype, const void *amax,
+                              int amax_dtype, int64_t axis_size, int64_t inner,
+                              hipStream_t stream);
+
+/* Unscaled e4m3 round trip, `_fp8_eager(x, amax=None)` (tensor_quant.py:55-59): torch's
+ * float8_e4m3fn cast, RNE, |x| > 464 (incl. inf) -> NaN (no saturation). */
+int mtq_e4m3_cast(const void *x, void *y, int64_t n, int dtype, hipStream_t stream);
+
+/* ---- dynamic block (MX) fake quant -------------------------------------------------------
+ * Replaces `fused_amax_convert` (tensor_quant_mx.cu:316-352 -> amax_and_convert_kernel
+ * :239-294).  Input viewed as [rows, cols] (cols = last dim); blocks of block_size along
+ * cols (a partial last block is zero-padded); per block amax = max|x| (inf clamps to
+ * FLT_MAX), scale from `scale_format` (E8M0 = the reference's NV rounding, :104-137;
+ * otherwise :139-183 in double), y = sign * convert(|x| * scale, format) * unscale.
+ * global_amax may be NULL; with per_channel != 0 it holds one fp32 value per row. */
+int mtq_fused_amax_convert(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
+                           int block_size, int format, int scale_format,
+                           const float *global_amax, int per_channel, hipStream_t stream);
+
+/* Host-side scalar conversion (reference `convert_to_exmy`, tensor_quant_mx.cu:399 ->
+ * convert_to_types, tensor_quant_mx.h:161-188). */
+float mtq_convert_to_exmy(float x, int format);
+
+/* ---- amax reductions ---------------------------------------------------------------------
+ * Accumulating max|x| reduction: out[k] = max(out[k], max_{p,q} |x[p, k, q]|) for x viewed
+ * as [P, K, Q] (dense).  NaN anywhere in a reduced set makes out[k] NaN (torch.max
+ * semantics).  `out` is fp32 and must be initialised by the caller (0 for a fresh
+ * reduction); accumulation across calls implements MaxCalibrator.collect's running max
+ * (calib/max.py:53-86 over reduce_amax, utils/core_utils.py:146-183) in one launch,
+ * without the reference's two passes (max, min) and host-syncing asserts. */
+int mtq_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtype, float *out,
+                    hipStream_t stream);
+
+/* Fused dynamic INT-n block quant with in-kernel block amax and an optional per-column
+ * pre-quant scale:  t = T(x * pqs[col]) (rounded to the input dtype, as the reference's
+ * `inputs * pre_quant_scale`, tensor_quantizer.py:1143-1144), per block of `block` along
+ * cols amax = max|t|, y = INT-n qdq(t, amax).  One HBM pass; this is the weight side of the
+ * AWQ-lite alpha search (model_calib.py:1540-1553) where the reference issues a multiply,
+ * two reductions and the qdq per alpha.  pqs may be NULL (no scaling); pqs_dtype as dtype. */
+int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
+                            const void *pqs, int pqs_dtype, int block, int num_bits,
+                            int is_unsigned, int narrow_range, hipStream_t stream);
+
+/* ---- histogram ---------------------------------------------------------------------------
+ * torch.histc(|x|, bins, min=0, max=*hmax) semantics (as used by HistogramCalibrator.collect,
+ * calib/histogram.py:108-130): bin = (int)((|x| * bins) / max) in fp32 (multiply, then
+ * divide), |x| == max -> last bin, |x| > max or NaN dropped; max == 0 widens the range to
+ * [-1, 1] like histc; skip_zeros drops exact zeros (calib/histogram.py:105-106).  Counts are
+ * accumulated into
+ * `counts` (uint32, caller-initialised) so repeated calls sum.  `hmax` is a device fp32
+ * scalar (no host sync). */
+int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, int bins,
+                      int skip_zeros, uint32_t *counts, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTQ_AMD_H_ */

@@ -1,0 +1,981 @@
+// mtq_kernels.hip — MI355X (gfx950, CDNA4) fake-quantization and calibration kernels and the
+// C ABI declared in include/mtq_amd.h.
+//
+// Design: every kernel here is HBM-bound (<= ~10 VALU ops per byte), so the
+// kernels are built around 16-byte-per-lane coalesced loads/stores, a grid of
+// min(work, 8 blocks x CUs) 256-thread blocks with a grid-stride loop and 4 vectors in flight
+// per lane, per-tensor/per-channel constants computed on the device (no host ATen scale ops,
+// unlike tensor_quant_gpu_fp8.cu:97-100), and wave64 shuffle reductions.  Reference citations
+// are relative to the reference repository root.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+
+#include "mtq_amd.h"
+#include "mtq_device.hpp"
+
+using namespace mtq;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+
+thread_local int g_last_hip_error = 0;
+
+int num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cu <= 0)
+      cu = 256;
+    cached[dev] = cu;
+  }
+  return cached[dev];
+}
+
+unsigned grid_for(int64_t work_items, int per_block) {
+  int64_t blocks = (work_items + per_block - 1) / per_block;
+  int64_t cap = (int64_t)num_cus() * 8;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  return (unsigned)blocks;
+}
+
+int check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_last_hip_error = (int)e;
+    return MTQ_ERR_LAUNCH;
+  }
+  return MTQ_OK;
+}
+
+FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) l++;
+  f.s = l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ============================================================================================
+// Element-wise driver: vectorised main body + scalar tail.  `Op` provides
+//   init()                       per-thread constants (per-tensor scale etc.)
+//   vec(Vec<T>&, int64_t vi)     quantise one 16-byte vector (vector index vi)
+//   one(float x, int64_t i)      quantise one element (element index i)
+// ============================================================================================
+template <typename T, class Op>
+__global__ __launch_bounds__(kThreads) void ew_vec_kernel(const T *__restrict__ x,
+                                                           T *__restrict__ y, int64_t nvec,
+                                                           Op op) {
+  using V = Vec<T>;
+  op.init();
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
+    V v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) v[u] = ldg_vec(x + (i + u * stride) * V::N);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) op.vec(v[u], i + u * stride);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) stg_vec(y + (i + u * stride) * V::N, v[u]);
+  }
+  for (; i < nvec; i += stride) {
+    V v = ldg_vec(x + i * V::N);
+    op.vec(v, i);
+    stg_vec(y + i * V::N, v);
+  }
+}
+
+template <typename T, class Op>
+__global__ __launch_bounds__(kThreads) void ew_scalar_kernel(const T *__restrict__ x,
+                                                              T *__restrict__ y, int64_t begin,
+                                                              int64_t n, Op op) {
+  op.init();
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = begin + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+    y[i] = Elem<T>::st(op.one(Elem<T>::ld(x[i]), i));
+}
+
+template <typename T, class Op>
+int launch_ew(const void *xv, void *yv, int64_t n, Op op, hipStream_t stream) {
+  const T *x = reinterpret_cast<const T *>(xv);
+  T *y = reinterpret_cast<T *>(yv);
+  if (n <= 0) return MTQ_OK;
+  constexpr int N = Vec<T>::N;
+  int64_t nvec = (aligned16(x) && aligned16(y)) ? n / N : 0;
+  if (nvec > 0) {
+    unsigned g = grid_for(nvec, kThreads * kUnroll);
+    ew_vec_kernel<T, Op><<<g, kThreads, 0, stream>>>(x, y, nvec, op);
+  }
+  int64_t done = nvec * N;
+  if (done < n) {
+    unsigned g = grid_for(n - done, kThreads);
+    ew_scalar_kernel<T, Op><<<g, kThreads, 0, stream>>>(x, y, done, n, op);
+  }
+  return check_launch();
+}
+
+// --------------------------------------------------------------------------------------------
+// INT-n ops
+// --------------------------------------------------------------------------------------------
+struct IntBounds {
+  float max_bound, min_bound;
+};
+IntBounds int_bounds(int num_bits, int is_unsigned, int narrow_range) {
+  // tensor_quant.py:624-632 / tensor_quant_gpu.cu:38-41,67-69
+  float mb = (float)((1ll << (num_bits - 1 + (is_unsigned ? 1 : 0))) - 1);
+  float lo = is_unsigned ? 0.f : (narrow_range ? -mb : -mb - 1.f);
+  return {mb, lo};
+}
+
+template <typename T> struct IntTensorOp {
+  const void *amax;
+  int amax_dtype;
+  float max_bound, min_bound;
+  IntQ q;
+  __device__ __forceinline__ void init() {
+    q = make_intq(load_as_float(amax, amax_dtype, 0), max_bound, min_bound);
+  }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t) {
+#pragma unroll
+    for (int j = 0; j < Vec<T>::N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
+  }
+  __device__ __forceinline__ float one(float x, int64_t) { return int_qdq(x, q); }
+};
+
+// Channel of vector vi when `inner` is a multiple of the vector width: all elements of the
+// vector share (vi / inner_vec) % axis_size.  Indices < 2^31 use the fast divider.
+template <typename T> struct IntAxisVecOp {
+  const void *amax;
+  int amax_dtype;
+  float max_bound, min_bound;
+  FastDiv inner_vec, axis;
+  bool small;
+  int64_t inner_vec64, axis64;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ int64_t chan(int64_t vi) const {
+    if (small) {
+      uint32_t r = fdiv((uint32_t)vi, inner_vec);
+      uint32_t q = fdiv(r, axis);
+      return r - q * axis.d;
+    }
+    return (vi / inner_vec64) % axis64;
+  }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) {
+    IntQ q = make_intq(load_as_float(amax, amax_dtype, chan(vi)), max_bound, min_bound);
+#pragma unroll
+    for (int j = 0; j < Vec<T>::N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
+  }
+  __device__ __forceinline__ float one(float x, int64_t i) {
+    int64_t c = (i / (inner_vec64 * Vec<T>::N)) % axis64;
+    return int_qdq(x, make_intq(load_as_float(amax, amax_dtype, c), max_bound, min_bound));
+  }
+};
+
+// Generic channel mapping (inner not a multiple of the vector width, e.g. axis = -1).
+template <typename T> struct IntAxisElemOp {
+  const void *amax;
+  int amax_dtype;
+  float max_bound, min_bound;
+  int64_t inner, axis;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ float one(float x, int64_t i) {
+    int64_t c = (i / inner) % axis;
+    return int_qdq(x, make_intq(load_as_float(amax, amax_dtype, c), max_bound, min_bound));
+  }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) {
+#pragma unroll
+    for (int j = 0; j < Vec<T>::N; ++j)
+      v.e[j] = Elem<T>::st(one(Elem<T>::ld(v.e[j]), vi * Vec<T>::N + j));
+  }
+};
+
+// --------------------------------------------------------------------------------------------
+// FP8 ops
+// --------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void fp8_vec(Vec<T> &v, const Fp8Q &q) {
+#pragma unroll
+  for (int j = 0; j < Vec<T>::N; j += 2) {
+    float a = Elem<T>::ld(v.e[j]);
+    float b = (j + 1 < Vec<T>::N) ? Elem<T>::ld(v.e[j + 1]) : 0.f;
+    fp8_qdq2(a, b, q);
+    v.e[j] = Elem<T>::st(a);
+    if (j + 1 < Vec<T>::N) v.e[j + 1] = Elem<T>::st(b);
+  }
+}
+__device__ __forceinline__ float fp8_one(float x, const Fp8Q &q) {
+  float b = 0.f;
+  fp8_qdq2(x, b, q);
+  return x;
+}
+
+template <typename T> struct Fp8TensorOp {
+  const void *amax;
+  int amax_dtype;
+  Fp8Q q;
+  __device__ __forceinline__ void init() { q = make_fp8q(load_as_float(amax, amax_dtype, 0)); }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t) { fp8_vec(v, q); }
+  __device__ __forceinline__ float one(float x, int64_t) { return fp8_one(x, q); }
+};
+
+template <typename T> struct Fp8AxisVecOp {
+  const void *amax;
+  int amax_dtype;
+  FastDiv inner_vec, axis;
+  bool small;
+  int64_t inner_vec64, axis64;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ int64_t chan(int64_t vi) const {
+    if (small) {
+      uint32_t r = fdiv((uint32_t)vi, inner_vec);
+      uint32_t q = fdiv(r, axis);
+      return r - q * axis.d;
+    }
+    return (vi / inner_vec64) % axis64;
+  }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) {
+    fp8_vec(v, make_fp8q(load_as_float(amax, amax_dtype, chan(vi))));
+  }
+  __device__ __forceinline__ float one(float x, int64_t i) {
+    int64_t c = (i / (inner_vec64 * Vec<T>::N)) % axis64;
+    return fp8_one(x, make_fp8q(load_as_float(amax, amax_dtype, c)));
+  }
+};
+
+template <typename T> struct Fp8AxisElemOp {
+  const void *amax;
+  int amax_dtype;
+  int64_t inner, axis;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ float one(float x, int64_t i) {
+    int64_t c = (i / inner) % axis;
+    return fp8_one(x, make_fp8q(load_as_float(amax, amax_dtype, c)));
+  }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) {
+#pragma unroll
+    for (int j = 0; j < Vec<T>::N; ++j)
+      v.e[j] = Elem<T>::st(one(Elem<T>::ld(v.e[j]), vi * Vec<T>::N + j));
+  }
+};
+
+// torch float8_e4m3fn cast (no clamp): |x| > 464 (the 448/480 midpoint) overflows to NaN.
+template <typename T> struct Fp8CastOp {
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ static float ovf(float v) {
+    return fabsf(v) > 464.0f ? __builtin_nanf("") : v;
+  }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t) {
+#pragma unroll
+    for (int j = 0; j < Vec<T>::N; j += 2) {
+      int p = __builtin_amdgcn_cvt_pk_fp8_f32(ovf(Elem<T>::ld(v.e[j])),
+                                              ovf(Elem<T>::ld(v.e[j + 1])), 0, false);
+      v.e[j] = Elem<T>::st(__builtin_amdgcn_cvt_f32_fp8(p, 0));
+      v.e[j + 1] = Elem<T>::st(__builtin_amdgcn_cvt_f32_fp8(p, 1));
+    }
+  }
+  __device__ __forceinline__ float one(float x, int64_t) {
+    int p = __builtin_amdgcn_cvt_pk_fp8_f32(ovf(x), 0.f, 0, false);
+    return __builtin_amdgcn_cvt_f32_fp8(p, 0);
+  }
+};
+
+// --------------------------------------------------------------------------------------------
+// Axis dispatch shared by INT and FP8
+// --------------------------------------------------------------------------------------------
+template <typename T, template <typename> class VecOp, template <typename> class ElemOp,
+          class Fill>
+int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t inner,
+                Fill fill, hipStream_t stream) {
+  constexpr int N = Vec<T>::N;
+  if (inner % N == 0) {
+    VecOp<T> op;
+    fill(op);
+    op.inner_vec64 = inner / N;
+    op.axis64 = axis_size;
+    op.small = (n / N) < (1ll << 31) && op.inner_vec64 < (1ll << 31) && axis_size < (1ll << 31);
+    if (op.small) {
+      op.inner_vec = make_fastdiv((uint32_t)op.inner_vec64);
+      op.axis = make_fastdiv((uint32_t)axis_size);
+    }
+    return launch_ew<T>(x, y, n, op, stream);
+  }
+  ElemOp<T> op;
+  fill(op);
+  op.inner = inner;
+  op.axis = axis_size;
+  return launch_ew<T>(x, y, n, op, stream);
+}
+
+template <class F> int dispatch_dtype(int dtype, F &&f) {
+  switch (dtype) {
+  case MTQ_F32: return f(float{});
+  case MTQ_F16: return f(_Float16{});
+  case MTQ_BF16: return f(__bf16{});
+  case MTQ_F64: return f(double{});
+  default: return MTQ_ERR_DTYPE;
+  }
+}
+
+template <class F> int dispatch_dtype_nof64(int dtype, F &&f) {
+  switch (dtype) {
+  case MTQ_F32: return f(float{});
+  case MTQ_F16: return f(_Float16{});
+  case MTQ_BF16: return f(__bf16{});
+  default: return MTQ_ERR_DTYPE;
+  }
+}
+
+bool valid_dtype(int d) { return d >= 0 && d <= 3; }
+
+// ============================================================================================
+// MX / dynamic-block kernel (amax_and_convert_kernel, tensor_quant_mx.cu:239-294)
+// ============================================================================================
+struct MxParams {
+  int fmt, sfmt;
+  const float *gamax;
+  int per_channel;
+  int64_t cols;
+};
+
+__device__ __forceinline__ void mx_block_scale(float bamax, int64_t row, const MxParams &p,
+                                               float &scale, float &unscale) {
+  if (p.gamax) {
+    float g = p.gamax[p.per_channel ? row : 0];
+    global_scale(g, bamax, p.fmt, p.sfmt, scale, unscale);
+  } else if (p.sfmt == MTQ_E8M0) {
+    e8m0_scale(bamax, format_max(p.fmt), scale, unscale);
+  } else {
+    generic_scale(bamax, p.fmt, p.sfmt, scale, unscale);
+  }
+}
+
+// quantize(), tensor_quant_mx.cu:36-55: sign * convert(|x| * scale) * unscale.
+__device__ __forceinline__ float mx_qdq(float x, float scale, float unscale, int fmt) {
+  float a = fabsf(x) * scale;
+  float c = convert_fmt(a, fmt) * unscale;
+  return x < 0.f ? -c : c;
+}
+
+// Fast path: cols % bs == 0 and 16-byte aligned rows, so blocks never straddle rows and the
+// tensor is a flat sequence of blocks.  LPB = lanes per block = bs / N (N elements per lane);
+// the block amax is a shuffle-max over LPB adjacent lanes (<= 8 lanes: one DPP row).
+template <typename T, int BS>
+__global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ x,
+                                                           T *__restrict__ y, int64_t nvec,
+                                                           MxParams p) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  constexpr int LPB = BS / N >= 1 ? BS / N : 1;
+  static_assert(BS % N == 0, "block must be a multiple of the vector");
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  // stride and the start index are multiples of LPB, so the LPB lanes of a block stay together
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i - (threadIdx.x % LPB) < nvec;
+       i += stride) {
+    const bool live = i < nvec;
+    V v;
+    if (live) v = ldg_vec(x + i * N);
+    float m = 0.f;
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) m = fmaxf(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
+    }
+    m = group_max_f<LPB>(m);
+    if (!live) continue;
+    const int64_t blk = i / LPB;
+    const int64_t row = (blk * BS) / p.cols;
+    float scale, unscale;
+    mx_block_scale(m, row, p, scale, unscale);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, p.fmt));
+    stg_vec(y + i * N, v);
+  }
+}
+
+// General path: one lane per element of the zero-padded [rows, padded_cols] matrix; BS lanes
+// per block (BS divides 64, so a block never straddles a wave).
+template <typename T, int BS>
+__global__ __launch_bounds__(kThreads) void mx_scalar_kernel(const T *__restrict__ x,
+                                                              T *__restrict__ y, int64_t rows,
+                                                              int64_t cols, int64_t pcols,
+                                                              MxParams p) {
+  const int64_t total = rows * pcols;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx - (threadIdx.x % BS) < total;
+       idx += stride) {
+    const bool live = idx < total;
+    int64_t row = live ? idx / pcols : 0;
+    int64_t col = live ? idx - row * pcols : 0;
+    bool real = live && col < cols;
+    float v = real ? Elem<T>::ld(x[row * cols + col]) : 0.f;
+    float m = group_max_f<BS>(clamp_flt_max(fabsf(v)));
+    if (!real) continue;
+    float scale, unscale;
+    mx_block_scale(m, row, p, scale, unscale);
+    y[row * cols + col] = Elem<T>::st(mx_qdq(v, scale, unscale, p.fmt));
+  }
+}
+
+template <typename T>
+int launch_mx(const void *xv, void *yv, int64_t rows, int64_t cols, int bs, MxParams p,
+              hipStream_t stream) {
+  const T *x = reinterpret_cast<const T *>(xv);
+  T *y = reinterpret_cast<T *>(yv);
+  if (rows <= 0 || cols <= 0) return MTQ_OK;
+  constexpr int N = Vec<T>::N;
+  const int64_t n = rows * cols;
+  if (cols % bs == 0 && bs % N == 0 && aligned16(x) && aligned16(y)) {
+    int64_t nvec = n / N;
+    unsigned g = grid_for(nvec, kThreads);
+    switch (bs) {
+    case 8: mx_vec_kernel<T, 8><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+    case 16: mx_vec_kernel<T, 16><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+    case 32: mx_vec_kernel<T, 32><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+    default: return MTQ_ERR_BLOCKSIZE;
+    }
+    return check_launch();
+  }
+  int64_t pcols = (cols + bs - 1) / bs * bs;
+  unsigned g = grid_for(rows * pcols, kThreads);
+  switch (bs) {
+  case 8: mx_scalar_kernel<T, 8><<<g, kThreads, 0, stream>>>(x, y, rows, cols, pcols, p); break;
+  case 16: mx_scalar_kernel<T, 16><<<g, kThreads, 0, stream>>>(x, y, rows, cols, pcols, p); break;
+  case 32: mx_scalar_kernel<T, 32><<<g, kThreads, 0, stream>>>(x, y, rows, cols, pcols, p); break;
+  default: return MTQ_ERR_BLOCKSIZE;
+  }
+  return check_launch();
+}
+
+// ============================================================================================
+// amax reductions (MaxCalibrator.collect / reduce_amax)
+// ============================================================================================
+template <typename T>
+__device__ __forceinline__ uint32_t vec_absmax_bits(const Vec<T> &v) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < Vec<T>::N; ++j) {
+    uint32_t b = abs_bits_t<T>(v.e[j]);
+    m = b > m ? b : m;
+  }
+  return m;
+}
+
+// Per-tensor (K = 1, Q = 1): grid-stride vector loop, wave max, block max in LDS, one
+// atomicMax per block on the fp32 bit pattern.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void amax_all_kernel(const T *__restrict__ x, int64_t n,
+                                                             int64_t nvec, uint32_t *out) {
+  using V = Vec<T>;
+  __shared__ uint32_t red[kThreads / 64];
+  uint32_t m = 0;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
+    V v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) v[u] = ldg_vec(x + (i + u * stride) * V::N);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      uint32_t b = vec_absmax_bits(v[u]);
+      m = b > m ? b : m;
+    }
+  }
+  for (; i < nvec; i += stride) {
+    uint32_t b = vec_absmax_bits(ldg_vec(x + i * V::N));
+    m = b > m ? b : m;
+  }
+  // scalar tail (n % N elements, or all of them when unaligned)
+  for (int64_t t = nvec * V::N + (int64_t)blockIdx.x * kThreads + threadIdx.x; t < n; t += stride) {
+    uint32_t b = abs_bits_t<T>(x[t]);
+    m = b > m ? b : m;
+  }
+  m = wave_max_u32(m);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 1; k < kThreads / 64; ++k) m = red[k] > m ? red[k] : m;
+    atomicMax(out, m);
+  }
+}
+
+// Rows: x viewed as [R, Q] contiguous rows (R = P*K), out[r % K].  G lanes per row (G = 64
+// for long rows, fewer for short ones), each row optionally split into `chunks` pieces handled
+// by different groups; one atomicMax per (row, chunk).
+template <typename T, int G>
+__global__ __launch_bounds__(kThreads) void amax_rows_kernel(const T *__restrict__ x, int64_t R,
+                                                              int64_t Q, int64_t K,
+                                                              int64_t chunk_vec, int64_t chunks,
+                                                              uint32_t *out) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t qvec = Q / N;
+  const int64_t items = R * chunks;
+  const int64_t groups_total = (int64_t)gridDim.x * (kThreads / G);
+  const int gl = threadIdx.x % G;
+  for (int64_t it = (int64_t)blockIdx.x * (kThreads / G) + threadIdx.x / G; it < items;
+       it += groups_total) {
+    const int64_t r = it / chunks, c = it - r * chunks;
+    const int64_t v0 = c * chunk_vec;
+    int64_t v1 = v0 + chunk_vec;
+    v1 = v1 < qvec ? v1 : qvec;
+    const T *row = x + r * Q;
+    uint32_t m = 0;
+    for (int64_t v = v0 + gl; v < v1; v += G) {
+      uint32_t b = vec_absmax_bits(ldg_vec(row + v * N));
+      m = b > m ? b : m;
+    }
+    m = group_max_u32<G>(m);
+    if (gl == 0) atomicMax(out + (r % K), m);
+  }
+}
+
+// Columns: x viewed as [P, K] (Q = 1, K % N == 0), out[k] over p.  Each lane owns one vector
+// of N consecutive columns and a slab of rows.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void amax_cols_kernel(const T *__restrict__ x, int64_t P,
+                                                              int64_t K, int64_t rows_per_slab,
+                                                              uint32_t *out) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t kvec = K / N;
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t slabs = (P + rows_per_slab - 1) / rows_per_slab;
+  if (t >= kvec * slabs) return;
+  const int64_t s = t / kvec, kv = t - s * kvec;
+  const int64_t p0 = s * rows_per_slab;
+  int64_t p1 = p0 + rows_per_slab;
+  p1 = p1 < P ? p1 : P;
+  uint32_t m[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) m[j] = 0;
+  for (int64_t p = p0; p < p1; ++p) {
+    V v = ldg_vec(x + p * K + kv * N);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      uint32_t b = abs_bits_t<T>(v.e[j]);
+      m[j] = b > m[j] ? b : m[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) atomicMax(out + kv * N + j, m[j]);
+}
+
+// Generic: one element per lane, atomicMax per element (any P, K, Q, alignment).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void amax_generic_kernel(const T *__restrict__ x,
+                                                                 int64_t n, int64_t K, int64_t Q,
+                                                                 uint32_t *out) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    int64_t k = (i / Q) % K;
+    atomicMax(out + k, abs_bits_t<T>(x[i]));
+  }
+}
+
+template <typename T>
+int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
+                hipStream_t stream) {
+  const T *x = reinterpret_cast<const T *>(xv);
+  uint32_t *out = reinterpret_cast<uint32_t *>(outf);
+  const int64_t n = P * K * Q;
+  if (n <= 0) return MTQ_OK;
+  constexpr int N = Vec<T>::N;
+  const bool al = aligned16(x);
+  if (K == 1 && (Q == 1 || P == 1)) {  // per-tensor
+    int64_t nvec = al ? n / N : 0;
+    unsigned g = grid_for(n / N + 1, kThreads * kUnroll * 4);
+    amax_all_kernel<T><<<g, kThreads, 0, stream>>>(x, n, nvec, out);
+    return check_launch();
+  }
+  if (Q % N == 0 && al && Q >= N) {
+    const int64_t R = P * K, qvec = Q / N;
+    // chunk long rows so that there are enough independent items to fill the chip
+    int64_t chunk_vec = qvec;
+    const int64_t want_items = (int64_t)num_cus() * 16;
+    if (R < want_items && qvec > 512) {
+      int64_t chunks = (want_items + R - 1) / R;
+      chunk_vec = (qvec + chunks - 1) / chunks;
+      chunk_vec = (chunk_vec + 63) / 64 * 64;
+    }
+    int64_t chunks = (qvec + chunk_vec - 1) / chunk_vec;
+    int64_t items = R * chunks;
+    if (chunk_vec >= 64) {
+      unsigned g = grid_for(items, kThreads / 64);
+      amax_rows_kernel<T, 64><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunk_vec, chunks, out);
+    } else if (chunk_vec >= 16) {
+      unsigned g = grid_for(items, kThreads / 16);
+      amax_rows_kernel<T, 16><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunk_vec, chunks, out);
+    } else {
+      unsigned g = grid_for(items, kThreads / 4);
+      amax_rows_kernel<T, 4><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunk_vec, chunks, out);
+    }
+    return check_launch();
+  }
+  if (Q == 1 && K % N == 0 && al) {
+    const int64_t kvec = K / N;
+    // enough slabs for ~16 waves per CU
+    int64_t want_threads = (int64_t)num_cus() * kThreads * 4;
+    int64_t slabs = (want_threads + kvec - 1) / kvec;
+    if (slabs > P) slabs = P;
+    if (slabs < 1) slabs = 1;
+    int64_t rows_per_slab = (P + slabs - 1) / slabs;
+    slabs = (P + rows_per_slab - 1) / rows_per_slab;
+    int64_t threads = kvec * slabs;
+    unsigned g = (unsigned)((threads + kThreads - 1) / kThreads);
+    amax_cols_kernel<T><<<g, kThreads, 0, stream>>>(x, P, K, rows_per_slab, out);
+    return check_launch();
+  }
+  unsigned g = grid_for(n, kThreads);
+  amax_generic_kernel<T><<<g, kThreads, 0, stream>>>(x, n, K, Q, out);
+  return check_launch();
+}
+
+// ============================================================================================
+// Dynamic INT-n block quant with optional per-column pre-quant scale (AWQ-lite weight side)
+// ============================================================================================
+template <typename T, int BLK>
+__global__ __launch_bounds__(kThreads) void block_quant_dyn_kernel(
+    const T *__restrict__ x, T *__restrict__ y, const T *__restrict__ pqs, int64_t nvec,
+    int64_t cols, float max_bound, float min_bound) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  constexpr int LPB = BLK / N;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i - (threadIdx.x % LPB) < nvec;
+       i += stride) {
+    const bool live = i < nvec;
+    V v;
+    uint32_t m = 0;
+    if (live) {
+      v = ldg_vec(x + i * N);
+      if (pqs) {
+        const int64_t col = (i * N) % cols;
+        V s = ldg_vec(pqs + col);
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+          v.e[j] = Elem<T>::st(Elem<T>::ld(v.e[j]) * Elem<T>::ld(s.e[j]));
+      }
+      m = vec_absmax_bits(v);
+    }
+    m = group_max_u32<LPB>(m);
+    if (!live) continue;
+    IntQ q = make_intq(__uint_as_float(m), max_bound, min_bound);
+#pragma unroll
+    for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
+    stg_vec(y + i * N, v);
+  }
+}
+
+// ============================================================================================
+// Histogram of |x| (torch.histc semantics, LDS-privatised)
+// ============================================================================================
+template <typename T>
+__global__ __launch_bounds__(kThreads) void hist_kernel(const T *__restrict__ x, int64_t n,
+                                                         const float *hmax, int bins,
+                                                         int skip_zeros, uint32_t *counts,
+                                                         int use_lds) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {  // histc_select_outer_bin_edges: widen a degenerate range by 1 on each side
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  const float fb = (float)bins;
+  const float span = hi - lo;
+  if (use_lds) {
+    for (int b = threadIdx.x; b < bins; b += kThreads) sh[b] = 0;
+    __syncthreads();
+  }
+  uint32_t *dst = use_lds ? sh : counts;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    float v = fabsf(Elem<T>::ld(x[i]));
+    if (skip_zeros && v == 0.f) continue;
+    if (!(v >= lo && v <= hi)) continue;  // outside the range or NaN
+    int b = (int)(((v - lo) * fb) / span);
+    if (b == bins) b -= 1;
+    atomicAdd(dst + b, 1u);
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < bins; b += kThreads)
+      if (sh[b]) atomicAdd(counts + b, sh[b]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void hist_vec_kernel(const T *__restrict__ x,
+                                                             int64_t nvec, const float *hmax,
+                                                             int bins, int skip_zeros,
+                                                             uint32_t *counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+  using V = Vec<T>;
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  const float fb = (float)bins;
+  const float span = hi - lo;
+  for (int b = threadIdx.x; b < bins; b += kThreads) sh[b] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride) {
+    V v = ldg_vec(x + i * V::N);
+#pragma unroll
+    for (int j = 0; j < V::N; ++j) {
+      float a = fabsf(Elem<T>::ld(v.e[j]));
+      bool ok = (a >= lo && a <= hi) && !(skip_zeros && a == 0.f);
+      if (ok) {
+        int b = (int)(((a - lo) * fb) / span);
+        if (b == bins) b -= 1;
+        atomicAdd(sh + b, 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < bins; b += kThreads)
+    if (sh[b]) atomicAdd(counts + b, sh[b]);
+}
+
+}  // namespace
+
+// ============================================================================================
+// C ABI
+// ============================================================================================
+extern "C" {
+
+const char *mtq_status_string(int status) {
+  switch (status) {
+  case MTQ_OK: return "ok";
+  case MTQ_ERR_INVALID_ARG: return "invalid argument";
+  case MTQ_ERR_DTYPE: return "unsupported dtype";
+  case MTQ_ERR_BLOCKSIZE: return "Blocksize for fused call must be one of {8, 16, 32}";
+  case MTQ_ERR_FORMAT: return "unsupported quantization format";
+  case MTQ_ERR_LAUNCH: return "HIP kernel launch failed";
+  case MTQ_ERR_NO_DEVICE: return "no HIP device";
+  default: return "unknown status";
+  }
+}
+
+int mtq_last_hip_error(void) { return g_last_hip_error; }
+
+int mtq_version(void) { return 100; }
+
+int mtq_fake_tensor_quant(const void *x, void *y, int64_t n, int dtype, const void *amax,
+                          int amax_dtype, int num_bits, int is_unsigned, int narrow_range,
+                          hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!x || !y || !amax)) || num_bits < 1 || num_bits > 31)
+    return MTQ_ERR_INVALID_ARG;
+  if (!valid_dtype(dtype) || !valid_dtype(amax_dtype)) return MTQ_ERR_DTYPE;
+  IntBounds b = int_bounds(num_bits, is_unsigned, narrow_range);
+  return dispatch_dtype(dtype, [&](auto t) {
+    using T = decltype(t);
+    IntTensorOp<T> op{amax, amax_dtype, b.max_bound, b.min_bound, {}};
+    return launch_ew<T>(x, y, n, op, stream);
+  });
+}
+
+int mtq_fake_tensor_quant_with_axis(const void *x, void *y, int64_t n, int dtype,
+                                    const void *amax, int amax_dtype, int64_t axis_size,
+                                    int64_t inner, int num_bits, int is_unsigned,
+                                    int narrow_range, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!x || !y || !amax)) || axis_size < 1 || inner < 1 || num_bits < 1 ||
+      num_bits > 31)
+    return MTQ_ERR_INVALID_ARG;
+  if (!valid_dtype(dtype) || !valid_dtype(amax_dtype)) return MTQ_ERR_DTYPE;
+  IntBounds b = int_bounds(num_bits, is_unsigned, narrow_range);
+  return dispatch_dtype(dtype, [&](auto t) {
+    using T = decltype(t);
+    auto fill = [&](auto &op) {
+      op.amax = amax;
+      op.amax_dtype = amax_dtype;
+      op.max_bound = b.max_bound;
+      op.min_bound = b.min_bound;
+    };
+    return launch_axis<T, IntAxisVecOp, IntAxisElemOp>(x, y, n, axis_size, inner, fill, stream);
+  });
+}
+
+int mtq_fake_e4m3fy(const void *x, void *y, int64_t n, int dtype, const void *amax,
+                    int amax_dtype, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!x || !y || !amax))) return MTQ_ERR_INVALID_ARG;
+  if (!valid_dtype(dtype) || !valid_dtype(amax_dtype)) return MTQ_ERR_DTYPE;
+  return dispatch_dtype(dtype, [&](auto t) {
+    using T = decltype(t);
+    Fp8TensorOp<T> op{amax, amax_dtype, {}};
+    return launch_ew<T>(x, y, n, op, stream);
+  });
+}
+
+int mtq_fake_e4m3fy_with_axis(const void *x, void *y, int64_t n, int dtype, const void *amax,
+                              int amax_dtype, int64_t axis_size, int64_t inner,
+                              hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!x || !y || !amax)) || axis_size < 1 || inner < 1)
+    return MTQ_ERR_INVALID_ARG;
+  if (!valid_dtype(dtype) || !valid_dtype(amax_dtype)) return MTQ_ERR_DTYPE;
+  return dispatch_dtype(dtype, [&](auto t) {
+    using T = decltype(t);
+    auto fill = [&](auto &op) {
+      op.amax = amax;
+      op.amax_dtype = amax_dtype;
+    };
+    return launch_axis<T, Fp8AxisVecOp, Fp8AxisElemOp>(x, y, n, axis_size, inner, fill, stream);
+  });
+}
+
+int mtq_e4m3_cast(const void *x, void *y, int64_t n, int dtype, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!x || !y))) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype(dtype, [&](auto t) {
+    using T = decltype(t);
+    return launch_ew<T>(x, y, n, Fp8CastOp<T>{}, stream);
+  });
+}
+
+int mtq_fused_amax_convert(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
+                           int block_size, int format, int scale_format,
+                           const float *global_amax, int per_channel, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || ((rows * cols) > 0 && (!x || !y))) return MTQ_ERR_INVALID_ARG;
+  if (block_size != 8 && block_size != 16 && block_size != 32) return MTQ_ERR_BLOCKSIZE;
+  if (format < 0 || format > 9 || scale_format < 0 || scale_format > 9) return MTQ_ERR_FORMAT;
+  MxParams p{format, scale_format, global_amax, per_channel, cols};
+  return dispatch_dtype_nof64(dtype, [&](auto t) {
+    using T = decltype(t);
+    return launch_mx<T>(x, y, rows, cols, block_size, p, stream);
+  });
+}
+
+int mtq_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtype, float *out,
+                    hipStream_t stream) {
+  if (P < 0 || K < 1 || Q < 0 || !out || (P * K * Q > 0 && !x)) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) {
+    using T = decltype(t);
+    return launch_amax<T>(x, P, K, Q, out, stream);
+  });
+}
+
+int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
+                            const void *pqs, int pqs_dtype, int block, int num_bits,
+                            int is_unsigned, int narrow_range, hipStream_t stream) {
+  if (rows < 0 || cols < 1 || num_bits < 1 || num_bits > 31) return MTQ_ERR_INVALID_ARG;
+  if (rows == 0) return MTQ_OK;
+  if (!x || !y) return MTQ_ERR_INVALID_ARG;
+  if (pqs && pqs_dtype != dtype) return MTQ_ERR_DTYPE;
+  IntBounds b = int_bounds(num_bits, is_unsigned, narrow_range);
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    if (cols % block != 0 || block % N != 0 || !aligned16(x) || !aligned16(y) ||
+        (pqs && !aligned16(pqs)))
+      return MTQ_ERR_INVALID_ARG;
+    const int64_t nvec = rows * cols / N;
+    unsigned g = grid_for(nvec, kThreads);
+    const T *xt = reinterpret_cast<const T *>(x);
+    T *yt = reinterpret_cast<T *>(y);
+    const T *pt = reinterpret_cast<const T *>(pqs);
+    switch (block) {
+    case 32:
+      block_quant_dyn_kernel<T, 32>
+          <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
+      break;
+    case 64:
+      block_quant_dyn_kernel<T, 64>
+          <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
+      break;
+    case 128:
+      block_quant_dyn_kernel<T, 128>
+          <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
+      break;
+    case 256:
+      if constexpr (N == 8) {
+        block_quant_dyn_kernel<T, 256>
+            <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
+        break;
+      }
+      return MTQ_ERR_BLOCKSIZE;
+    default: return MTQ_ERR_BLOCKSIZE;
+    }
+    return check_launch();
+  });
+}
+
+int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, int bins,
+                      int skip_zeros, uint32_t *counts, hipStream_t stream) {
+  if (n < 0 || bins < 1 || !hmax || !counts || (n > 0 && !x)) return MTQ_ERR_INVALID_ARG;
+  if (n == 0) return MTQ_OK;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    const T *xt = reinterpret_cast<const T *>(x);
+    const bool lds = bins <= 16384;
+    const size_t shm = lds ? (size_t)bins * 4 : 0;
+    if (lds && aligned16(x) && n % N == 0) {
+      unsigned g = grid_for(n / N, kThreads * 8);
+      hist_vec_kernel<T><<<g, kThreads, shm, stream>>>(xt, n / N, hmax, bins, skip_zeros, counts);
+    } else {
+      unsigned g = grid_for(n, kThreads * 8);
+      hist_kernel<T><<<g, kThreads, shm, stream>>>(xt, n, hmax, bins, skip_zeros, counts,
+                                                   lds ? 1 : 0);
+    }
+    return check_launch();
+  });
+}
+
+// Host restatement of convert_to_types (tensor_quant_mx.h:161-188) on the same minifloat
+// rounding rule the device uses; E4M3/E5M2 are the satfinite RNE casts.
+float mtq_convert_to_exmy(float x, int format) {
+  struct F {
+    int m, emin;
+    float vmax;
+    bool away;
+  };
+  F f;
+  switch (format) {
+  case MTQ_E4M3: f = {3, -6, 448.f, false}; break;
+  case MTQ_E5M2: f = {2, -14, 57344.f, false}; break;
+  case MTQ_INT8: {
+    float r = rintf(x);
+    return r > 127.f ? 127.f : (r < -127.f ? -127.f : r);
+  }
+  case MTQ_E0M3: f = {3, 3, 7.f, false}; break;
+  case MTQ_E1M2: f = {2, 1, 3.5f, false}; break;
+  case MTQ_E3M0: f = {0, -2, 16.f, true}; break;
+  case MTQ_E2M1: f = {1, 0, 6.f, false}; break;
+  case MTQ_E3M2: f = {2, -2, 28.f, false}; break;
+  case MTQ_E2M3: f = {3, 0, 7.5f, false}; break;
+  default: return 0.f;
+  }
+  if (x != x) {
+    if (format == MTQ_E4M3 || format == MTQ_E5M2) return x;
+    return f.vmax;  // table formats saturate NaN (sign of NaN is not negative)
+  }
+  float sign = x < 0.f ? -1.f : 1.f;
+  float v = fabsf(x);
+  v = v < f.vmax ? v : f.vmax;
+  uint32_t bits;
+  memcpy(&bits, &v, 4);
+  int e = (int)((bits >> 23) & 0xff) - 127;
+  if (e < f.emin) e = f.emin;
+  int k = e - f.m;
+  float t = ldexpf(v, -k);
+  float r = f.away ? floorf(t + 0.5f) : rintf(t);
+  r = ldexpf(r, k);
+  r = r < f.vmax ? r : f.vmax;
+  return sign * r;
+}
+
+}  // extern "C"

@@ -1,0 +1,405 @@
+// torch_ops.cpp — PyTorch-ROCm custom ops over the C ABI of libmtq_amd.so.
+//
+// Registers, under the `modelopt_amd` namespace, the op schemas of the reference's
+// torch.library ops (tensorrt::quantize_op / tensorrt::dynamic_block_quantize_op,
+// modelopt/torch/quantization/tensor_quant.py:222-276) and of its pybind extension modules
+// (modelopt_cuda_ext, tensor_quant.cpp:63-76; modelopt_cuda_ext_fp8,
+// tensor_quant_gpu_fp8.cu:109-114; modelopt_cuda_ext_mx, tensor_quant_mx.cu:393-411), plus
+// the calibration reductions.  Only the device ("CUDA" dispatch key = HIP on ROCm) and Meta
+// keys are implemented: there is no CPU compute path in the product, a CPU tensor raises.
+// Every kernel runs on the caller's current HIP stream; nothing here synchronises.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "mtq_amd.h"
+
+namespace {
+
+hipStream_t cur_stream(const at::Tensor &t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+int dtype_code(at::ScalarType s) {
+  switch (s) {
+  case at::kFloat: return MTQ_F32;
+  case at::kHalf: return MTQ_F16;
+  case at::kBFloat16: return MTQ_BF16;
+  case at::kDouble: return MTQ_F64;
+  default: return -1;
+  }
+}
+
+void check_status(int st, const char *what) {
+  if (st == MTQ_ERR_BLOCKSIZE) TORCH_CHECK_VALUE(false, what, ": ", mtq_status_string(st));
+  TORCH_CHECK(st == MTQ_OK, what, ": ", mtq_status_string(st),
+              st == MTQ_ERR_LAUNCH ? " (hipError " : "",
+              st == MTQ_ERR_LAUNCH ? std::to_string(mtq_last_hip_error()) : std::string(),
+              st == MTQ_ERR_LAUNCH ? ")" : "");
+}
+
+void check_device(const at::Tensor &t, const char *name) {
+  TORCH_CHECK(t.is_cuda(), "modelopt_amd: ", name,
+              " must be on a ROCm (HIP) device; the MI355X-native path has no CPU kernels");
+}
+
+int checked_dtype(const at::Tensor &t, const char *name) {
+  int d = dtype_code(t.scalar_type());
+  TORCH_CHECK(d >= 0, "modelopt_amd: unsupported dtype ", t.scalar_type(), " for ", name);
+  return d;
+}
+
+// amax -> (axis_size, inner) on the contiguous input, numpy-broadcast aligned to the input's
+// trailing dims.  The non-singleton dims of amax must form one contiguous run of input dims
+// (the reference's single-axis ext path, tensor_quant.py:85-91 / :103-108, is the one-dim case;
+// a run such as amax [B, T, 1] on input [B, T, H] merges into one axis).
+struct AxisMap {
+  bool per_tensor;
+  int64_t axis_size, inner;
+};
+
+AxisMap axis_map(const at::Tensor &x, const at::Tensor &amax) {
+  if (amax.numel() == 1) return {true, 1, 1};
+  const int64_t xd = x.dim(), ad = amax.dim();
+  TORCH_CHECK(ad <= xd, "modelopt_amd: amax of rank ", ad, " does not broadcast to input of rank ",
+              xd);
+  int first = -1, last = -1;
+  for (int64_t i = 0; i < ad; ++i) {
+    const int64_t xi = xd - ad + i;
+    if (amax.size(i) != 1) {
+      TORCH_CHECK(amax.size(i) == x.size(xi), "modelopt_amd: amax shape ", amax.sizes(),
+                  " does not broadcast to input shape ", x.sizes());
+      if (first < 0) first = (int)xi;
+      TORCH_CHECK(last < 0 || last == xi - 1,
+                  "modelopt_amd: amax with non-adjacent quantization axes is not supported (shape ",
+                  amax.sizes(), ")");
+      last = (int)xi;
+    }
+  }
+  int64_t axis_size = 1, inner = 1;
+  for (int i = first; i <= last; ++i) axis_size *= x.size(i);
+  for (int64_t i = last + 1; i < xd; ++i) inner *= x.size(i);
+  return {false, axis_size, inner};
+}
+
+at::Tensor amax_operand(const at::Tensor &amax, const at::Tensor &x) {
+  at::Tensor a = amax;
+  if (a.device() != x.device()) a = a.to(x.device());
+  if (!a.is_contiguous()) a = a.contiguous();
+  if (dtype_code(a.scalar_type()) < 0) a = a.to(at::kFloat);
+  return a;
+}
+
+// ---- INT ---------------------------------------------------------------------------------------
+void int_qdq_into(const at::Tensor &x, at::Tensor &y, const at::Tensor &amax_in, int64_t num_bits,
+                  bool is_unsigned, bool narrow_range) {
+  check_device(x, "inputs");
+  const int dt = checked_dtype(x, "inputs");
+  at::Tensor amax = amax_operand(amax_in, x);
+  AxisMap m = axis_map(x, amax);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st;
+  if (m.per_tensor)
+    st = mtq_fake_tensor_quant(x.data_ptr(), y.data_ptr(), x.numel(), dt, amax.data_ptr(),
+                               dtype_code(amax.scalar_type()), (int)num_bits, is_unsigned,
+                               narrow_range, cur_stream(x));
+  else
+    st = mtq_fake_tensor_quant_with_axis(x.data_ptr(), y.data_ptr(), x.numel(), dt,
+                                         amax.data_ptr(), dtype_code(amax.scalar_type()),
+                                         m.axis_size, m.inner, (int)num_bits, is_unsigned,
+                                         narrow_range, cur_stream(x));
+  check_status(st, "fake_tensor_quant");
+}
+
+at::Tensor fake_tensor_quant(const at::Tensor &inputs, const at::Tensor &amax, int64_t num_bits,
+                             bool is_unsigned, bool narrow_range) {
+  TORCH_CHECK(amax.numel() == 1, "fake_tensor_quant expects a per-tensor amax");
+  at::Tensor x = inputs.contiguous();
+  at::Tensor y = at::empty_like(x);
+  int_qdq_into(x, y, amax, num_bits, is_unsigned, narrow_range);
+  return y;
+}
+
+void fake_tensor_quant_(at::Tensor inputs, const at::Tensor &amax, int64_t num_bits,
+                        bool is_unsigned, bool narrow_range) {
+  TORCH_CHECK(inputs.is_contiguous(), "fake_tensor_quant_ requires a contiguous tensor");
+  TORCH_CHECK(amax.numel() == 1, "fake_tensor_quant_ expects a per-tensor amax");
+  int_qdq_into(inputs, inputs, amax, num_bits, is_unsigned, narrow_range);
+}
+
+at::Tensor fake_tensor_quant_with_axis(const at::Tensor &inputs, const at::Tensor &amax,
+                                       int64_t axis, int64_t num_bits, bool is_unsigned,
+                                       bool narrow_range) {
+  at::Tensor x = inputs.contiguous();
+  const int64_t ax = axis < 0 ? axis + x.dim() : axis;
+  TORCH_CHECK(ax >= 0 && ax < x.dim(), "axis out of range");
+  TORCH_CHECK(amax.numel() == x.size(ax), "amax must have size(axis) elements");
+  check_device(x, "inputs");
+  at::Tensor a = amax_operand(amax, x);
+  at::Tensor y = at::empty_like(x);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_fake_tensor_quant_with_axis(
+      x.data_ptr(), y.data_ptr(), x.numel(), checked_dtype(x, "inputs"), a.data_ptr(),
+      dtype_code(a.scalar_type()), x.size(ax), x.stride(ax), (int)num_bits, is_unsigned,
+      narrow_range, cur_stream(x));
+  check_status(st, "fake_tensor_quant_with_axis");
+  return y;
+}
+
+// ---- FP8 -----------------------------------------------------------------------------------
+at::Tensor fp8_qdq(const at::Tensor &inputs, const at::Tensor &amax_in) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  const int dt = checked_dtype(x, "inputs");
+  at::Tensor amax = amax_operand(amax_in, x);
+  AxisMap m = axis_map(x, amax);
+  at::Tensor y = at::empty_like(x);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st;
+  if (m.per_tensor)
+    st = mtq_fake_e4m3fy(x.data_ptr(), y.data_ptr(), x.numel(), dt, amax.data_ptr(),
+                         dtype_code(amax.scalar_type()), cur_stream(x));
+  else
+    st = mtq_fake_e4m3fy_with_axis(x.data_ptr(), y.data_ptr(), x.numel(), dt, amax.data_ptr(),
+                                   dtype_code(amax.scalar_type()), m.axis_size, m.inner,
+                                   cur_stream(x));
+  check_status(st, "fake_e4m3fy");
+  return y;
+}
+
+at::Tensor fake_e4m3fy(const at::Tensor &inputs, const at::Tensor &amax) {
+  TORCH_CHECK(amax.numel() == 1, "fake_e4m3fy expects a per-tensor amax");
+  return fp8_qdq(inputs, amax);
+}
+
+at::Tensor fake_e4m3fy_with_axis(const at::Tensor &inputs, const at::Tensor &amax, int64_t axis) {
+  at::Tensor x = inputs.contiguous();
+  const int64_t ax = axis < 0 ? axis + x.dim() : axis;
+  TORCH_CHECK(ax >= 0 && ax < x.dim(), "axis out of range");
+  TORCH_CHECK(amax.numel() == x.size(ax), "amax must have size(axis) elements");
+  check_device(x, "inputs");
+  at::Tensor a = amax_operand(amax, x);
+  at::Tensor y = at::empty_like(x);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_fake_e4m3fy_with_axis(x.data_ptr(), y.data_ptr(), x.numel(),
+                                     checked_dtype(x, "inputs"), a.data_ptr(),
+                                     dtype_code(a.scalar_type()), x.size(ax), x.stride(ax),
+                                     cur_stream(x));
+  check_status(st, "fake_e4m3fy_with_axis");
+  return y;
+}
+
+// plain e4m3 cast round trip (`_fp8_eager` with amax=None, tensor_quant.py:55-59).
+at::Tensor e4m3_cast(const at::Tensor &inputs) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  at::Tensor y = at::empty_like(x);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_e4m3_cast(x.data_ptr(), y.data_ptr(), x.numel(), checked_dtype(x, "inputs"),
+                             cur_stream(x)),
+               "e4m3_cast");
+  return y;
+}
+
+// ---- dynamic block (MX) ----------------------------------------------------------------------
+at::Tensor fused_amax_convert(const at::Tensor &inputs, int64_t block_size, int64_t format,
+                              int64_t scale_format, const c10::optional<at::Tensor> &global_amax) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  const int dt = checked_dtype(x, "inputs");
+  TORCH_CHECK(dt != MTQ_F64, "fused_amax_convert: float64 not implemented");
+  at::Tensor y = at::empty_like(x);
+  if (x.numel() == 0) return y;
+  const int64_t cols = x.dim() == 0 ? 1 : x.size(-1);
+  const int64_t rows = x.numel() / cols;
+  at::Tensor g;
+  bool per_channel = false;
+  if (global_amax.has_value() && global_amax->defined()) {
+    g = global_amax->to(x.device(), at::kFloat).contiguous();
+    // get_global_scaling, tensor_quant_mx.cu:296-312
+    per_channel = x.dim() == 2 && g.numel() == x.size(0);
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_fused_amax_convert(x.data_ptr(), y.data_ptr(), rows, cols, dt, (int)block_size,
+                                  (int)format, (int)scale_format,
+                                  g.defined() ? g.data_ptr<float>() : nullptr, per_channel ? 1 : 0,
+                                  cur_stream(x));
+  check_status(st, "fused_amax_convert");
+  return y;
+}
+
+// ---- reductions ---------------------------------------------------------------------------------
+// out (fp32, contiguous, K elements) = max(out, max_{p,q} |x[p,k,q]|)
+void amax_accumulate(const at::Tensor &inputs, at::Tensor out, int64_t P, int64_t K, int64_t Q) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == K,
+              "amax_accumulate: out must be a contiguous fp32 tensor with K elements");
+  TORCH_CHECK(P * K * Q == x.numel(), "amax_accumulate: view [P,K,Q] does not match numel");
+  int dt = checked_dtype(x, "inputs");
+  at::Tensor xx = x;
+  if (dt == MTQ_F64) {  // exactness for doubles is lost in fp32; upcast path not provided
+    TORCH_CHECK(false, "amax_accumulate: float64 inputs are not supported by the HIP reduction");
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_reduce_amax(xx.data_ptr(), P, K, Q, dt, out.data_ptr<float>(), cur_stream(x));
+  check_status(st, "reduce_amax");
+}
+
+at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at::Tensor> &pqs,
+                               int64_t block, int64_t num_bits, bool is_unsigned,
+                               bool narrow_range) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  const int dt = checked_dtype(x, "inputs");
+  at::Tensor y = at::empty_like(x);
+  const int64_t cols = x.size(-1), rows = x.numel() / cols;
+  at::Tensor s;
+  if (pqs.has_value() && pqs->defined()) {
+    s = pqs->to(x.device(), x.scalar_type()).contiguous();
+    TORCH_CHECK(s.numel() == cols, "block_quant_dynamic: pre_quant_scale must have cols elements");
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_block_quant_dynamic(x.data_ptr(), y.data_ptr(), rows, cols, dt,
+                                   s.defined() ? s.data_ptr() : nullptr, dt, (int)block,
+                                   (int)num_bits, is_unsigned, narrow_range, cur_stream(x));
+  check_status(st, "block_quant_dynamic");
+  return y;
+}
+
+void histogram_abs_accumulate(const at::Tensor &inputs, const at::Tensor &hmax, at::Tensor counts,
+                              int64_t bins, bool skip_zeros) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.is_contiguous() && counts.numel() >= bins,
+              "histogram: counts must be a contiguous int32 tensor with >= bins elements");
+  TORCH_CHECK(hmax.scalar_type() == at::kFloat && hmax.numel() == 1, "histogram: hmax fp32 scalar");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_histogram_abs(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"),
+                             hmax.data_ptr<float>(), (int)bins, skip_zeros ? 1 : 0,
+                             reinterpret_cast<uint32_t *>(counts.data_ptr<int32_t>()),
+                             cur_stream(x));
+  check_status(st, "histogram_abs");
+}
+
+// ---- reference torch.library ops (tensor_quant.py:115-195) -------------------------------------
+at::Tensor quantize_op(const at::Tensor &input, const at::Tensor &amax, int64_t num_bits,
+                       int64_t exponent_bits, bool is_unsigned, bool narrow_range) {
+  if (num_bits == 8 && exponent_bits == 4) return fp8_qdq(input, amax);
+  TORCH_CHECK_VALUE(exponent_bits == 0, "Invalid combination of (num_bits, exponent_bits): (",
+                    num_bits, ", ", exponent_bits, ").");
+  at::Tensor x = input.contiguous();
+  at::Tensor y = at::empty_like(x);
+  int_qdq_into(x, y, amax, num_bits, is_unsigned, narrow_range);
+  return y;
+}
+
+int format_code(int64_t e, int64_t m, bool is_int) {
+  if (is_int) return e == 8 ? MTQ_INT8 : -1;  // mx_format_map key 8
+  if (e == 4 && m == 3) return MTQ_E4M3;
+  if (e == 5 && m == 2) return MTQ_E5M2;
+  if (e == 3 && m == 2) return MTQ_E3M2;
+  if (e == 2 && m == 3) return MTQ_E2M3;
+  if (e == 8 && m == 0) return MTQ_E8M0;
+  if (e == 2 && m == 1) return MTQ_E2M1;
+  if (e == 1 && m == 2) return MTQ_E1M2;
+  if (e == 0 && m == 3) return MTQ_E0M3;
+  if (e == 3 && m == 0) return MTQ_E3M0;
+  return -1;
+}
+
+at::Tensor dynamic_block_quantize_op(const at::Tensor &input, int64_t block_size,
+                                     const c10::optional<at::Tensor> &amax, int64_t num_bits,
+                                     int64_t exponent_bits, int64_t scale_num_bits,
+                                     int64_t scale_exponent_bits) {
+  // _dynamic_block_quantize_impl, tensor_quant.py:157-195
+  const int64_t se = scale_exponent_bits, sm = scale_num_bits - scale_exponent_bits - 1;
+  int fmt;
+  if (exponent_bits != 0)
+    fmt = format_code(exponent_bits, num_bits - exponent_bits - 1, false);
+  else
+    fmt = format_code(num_bits, 0, true);
+  TORCH_CHECK(fmt >= 0, "Unsupported num_bits: ", num_bits, ", exponent_bits: ", exponent_bits,
+              " for dynamic block quantization.");
+  const int sfmt = format_code(se, sm, false);
+  TORCH_CHECK(sfmt >= 0, "Scale bits (", se, ", ", sm, ") are not a supported format");
+  c10::optional<at::Tensor> g;
+  if (sfmt != MTQ_E8M0) {
+    TORCH_CHECK(amax.has_value() && amax->defined() && amax->is_cuda(),
+                "amax must be a CUDA tensor for dynamic block quantization.");
+    g = amax->numel() != 1 ? amax->amax() : *amax;
+  }
+  return fused_amax_convert(input, block_size, fmt, sfmt, g);
+}
+
+at::Tensor meta_like(const at::Tensor &x) { return at::empty_like(x); }
+
+}  // namespace
+
+TORCH_LIBRARY(modelopt_amd, m) {
+  m.def("quantize_op(Tensor input, Tensor amax, int num_bits, int exponent_bits, bool unsigned, "
+        "bool narrow_range) -> Tensor");
+  m.def("dynamic_block_quantize_op(Tensor input, int block_size, Tensor? amax, int num_bits, "
+        "int exponent_bits, int scale_num_bits, int scale_exponent_bits) -> Tensor");
+  m.def("fake_tensor_quant(Tensor inputs, Tensor amax, int num_bits=8, bool unsigned=False, "
+        "bool narrow_range=True) -> Tensor");
+  m.def("fake_tensor_quant_(Tensor(a!) inputs, Tensor amax, int num_bits=8, bool unsigned=False, "
+        "bool narrow_range=True) -> ()");
+  m.def("fake_tensor_quant_with_axis(Tensor inputs, Tensor amax, int axis, int num_bits=8, "
+        "bool unsigned=False, bool narrow_range=True) -> Tensor");
+  m.def("fake_e4m3fy(Tensor inputs, Tensor amax) -> Tensor");
+  m.def("fake_e4m3fy_with_axis(Tensor inputs, Tensor amax, int axis) -> Tensor");
+  m.def("e4m3_cast(Tensor inputs) -> Tensor");
+  m.def("fused_amax_convert(Tensor inputs, int block_size, int format, int scale_format, "
+        "Tensor? global_amax=None) -> Tensor");
+  m.def("amax_accumulate(Tensor inputs, Tensor(a!) out, int P, int K, int Q) -> ()");
+  m.def("block_quant_dynamic(Tensor inputs, Tensor? pre_quant_scale, int block, int num_bits, "
+        "bool unsigned, bool narrow_range) -> Tensor");
+  m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
+        "bool skip_zeros) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
+  m.impl("quantize_op", &quantize_op);
+  m.impl("dynamic_block_quantize_op", &dynamic_block_quantize_op);
+  m.impl("fake_tensor_quant", &fake_tensor_quant);
+  m.impl("fake_tensor_quant_", &fake_tensor_quant_);
+  m.impl("fake_tensor_quant_with_axis", &fake_tensor_quant_with_axis);
+  m.impl("fake_e4m3fy", &fake_e4m3fy);
+  m.impl("fake_e4m3fy_with_axis", &fake_e4m3fy_with_axis);
+  m.impl("e4m3_cast", &e4m3_cast);
+  m.impl("fused_amax_convert", &fused_amax_convert);
+  m.impl("amax_accumulate", &amax_accumulate);
+  m.impl("block_quant_dynamic", &block_quant_dynamic);
+  m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);
+}
+
+TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
+  m.impl("quantize_op", [](const at::Tensor &x, const at::Tensor &, int64_t, int64_t, bool, bool) {
+    return meta_like(x);
+  });
+  m.impl("dynamic_block_quantize_op",
+         [](const at::Tensor &x, int64_t, const c10::optional<at::Tensor> &, int64_t, int64_t,
+            int64_t, int64_t) { return meta_like(x); });
+  m.impl("fake_tensor_quant",
+         [](const at::Tensor &x, const at::Tensor &, int64_t, bool, bool) { return meta_like(x); });
+  m.impl("fake_tensor_quant_with_axis",
+         [](const at::Tensor &x, const at::Tensor &, int64_t, int64_t, bool, bool) {
+           return meta_like(x);
+         });
+  m.impl("fake_e4m3fy", [](const at::Tensor &x, const at::Tensor &) { return meta_like(x); });
+  m.impl("fake_e4m3fy_with_axis",
+         [](const at::Tensor &x, const at::Tensor &, int64_t) { return meta_like(x); });
+  m.impl("e4m3_cast", [](const at::Tensor &x) { return meta_like(x); });
+  m.impl("fused_amax_convert",
+         [](const at::Tensor &x, int64_t, int64_t, int64_t, const c10::optional<at::Tensor> &) {
+           return meta_like(x);
+         });
+  m.impl("block_quant_dynamic",
+         [](const at::Tensor &x, const c10::optional<at::Tensor> &, int64_t, int64_t, bool, bool) {
+           return meta_like(x);
+         });
+}

@@ -1,0 +1,331 @@
+"""HIP kernels (through the torch ops over the C ABI) vs the CPU oracle, bit for bit.
+
+Mirrors the reference's two-oracle pattern (tests/gpu/torch/quantization/test_tensor_quant_cuda.py:
+ext == ATen path bit-exact for INT, FP8 ext == fp8_eager): here HIP == oracle/ref_ops.py, and the
+oracle itself is pinned to the reference by tests/test_oracle_golden.py.
+"""
+
+import math
+
+import pytest
+import torch
+
+from oracle import ref_ops as R
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [torch.float32, torch.float16, torch.bfloat16]
+
+
+def same_bits(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Bitwise equality, NaN == NaN (any payload); -0 vs +0 distinguished."""
+    a = a.detach().cpu()
+    b = b.detach().cpu()
+    if a.shape != b.shape or a.dtype != b.dtype:
+        return False
+    nan = torch.isnan(a.float()) & torch.isnan(b.float())
+    if a.dtype == torch.float64:
+        ia, ib = a.view(torch.int64), b.view(torch.int64)
+    elif a.dtype == torch.float32:
+        ia, ib = a.view(torch.int32), b.view(torch.int32)
+    else:
+        ia, ib = a.view(torch.int16), b.view(torch.int16)
+    return bool(((ia == ib) | nan).all())
+
+
+def mismatch(a, b):
+    a = a.detach().cpu().float()
+    b = b.detach().cpu().float()
+    bad = ~((a == b) | (torch.isnan(a) & torch.isnan(b)))
+    idx = bad.nonzero()[:5]
+    return f"{int(bad.sum())} mismatches, e.g. at {idx.tolist()}: {a[bad][:5].tolist()} vs {b[bad][:5].tolist()}"
+
+
+def rand_with_edges(shape, dtype, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(shape, generator=g) * scale
+    flat = x.view(-1)
+    n = flat.numel()
+    # half-way points for rounding ties, signed zeros, big outliers
+    k = max(1, n // 64)
+    flat[:k] = torch.round(flat[:k] * 8) / 8 + 0.5 / 8
+    flat[k : 2 * k] = 0.0
+    flat[2 * k : 3 * k] = -0.0
+    flat[3 * k] = 7.5 * scale
+    return x.to(dtype)
+
+
+def ops():
+    from modelopt_amd import _ext
+
+    return _ext.ops()
+
+
+# --------------------------------------------------------------------------------------------
+# INT
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("num_bits", [3, 4, 5, 7, 8, 11])
+@pytest.mark.parametrize("unsigned,narrow", [(False, True), (False, False), (True, False)])
+def test_int_per_tensor(gpu, dtype, num_bits, unsigned, narrow):
+    x = rand_with_edges((37, 129), dtype, seed=num_bits)
+    if unsigned:
+        x = x.abs()
+    amax = x.float().abs().amax() * 0.7
+    ref = R.tensor_quant(x, amax, num_bits, unsigned, narrow)
+    out = ops().fake_tensor_quant(x.to(gpu), amax.to(gpu), num_bits, unsigned, narrow)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_int_vectorised_and_tail(gpu, dtype):
+    # large enough for the unrolled vector loop, odd length for the scalar tail
+    x = rand_with_edges((1 << 20) + 3, dtype, seed=5)
+    amax = torch.tensor(2.5)
+    ref = R.tensor_quant(x, amax, 8, False, False)
+    out = ops().fake_tensor_quant(x.to(gpu), amax.to(gpu), 8, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+    # unaligned view (offset by one element) takes the scalar path
+    xs = x[1:]
+    out = ops().fake_tensor_quant(x.to(gpu)[1:], amax.to(gpu), 8, False, False)
+    ref = R.tensor_quant(xs, amax, 8, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+@pytest.mark.parametrize("amax_val", [0.0, 2.0**-24, 2.0**-25, 1e-30])
+def test_int_zero_amax(gpu, amax_val):
+    x = torch.tensor([1.0, -1.0, 0.0, -0.0, float("nan"), float("inf")], dtype=torch.float32)
+    amax = torch.tensor(amax_val)
+    ref = R.tensor_quant(x, amax, 8)
+    out = ops().fake_tensor_quant(x.to(gpu), amax.to(gpu), 8, False, True)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_int_special_values(gpu):
+    x = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e30, -1e30, 0.0, -0.0, 3.5, -3.5])
+    amax = torch.tensor(7.0)
+    ref = R.tensor_quant(x, amax, 4, False, False)
+    out = ops().fake_tensor_quant(x.to(gpu), amax.to(gpu), 4, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize(
+    "shape,amax_shape",
+    [
+        ((64, 256), (64, 1)),  # per-row (weight axis 0)
+        ((64, 256), (1, 256)),  # per-column (axis -1): element-wise channel path
+        ((4, 6, 40), (1, 6, 1)),  # middle axis
+        ((4, 6, 40), (4, 6, 1)),  # merged leading axes (per-token)
+        ((4096, 128), (4096, 1)),  # block-128 view of a weight
+        ((33, 24), (33, 1)),  # inner 24 = 3 bf16 vectors
+    ],
+)
+def test_int_axis(gpu, dtype, shape, amax_shape):
+    x = rand_with_edges(shape, dtype, seed=11)
+    g = torch.Generator().manual_seed(3)
+    amax = torch.rand(amax_shape, generator=g) * 3 + 0.1
+    amax.view(-1)[0] = 0.0  # one zero-amax channel
+    ref = R.tensor_quant(x, amax, 8, False, False)
+    out = ops().quantize_op(x.to(gpu), amax.to(gpu), 8, 0, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_int_with_axis_api(gpu):
+    x = rand_with_edges((48, 96), torch.bfloat16, seed=2)
+    amax = torch.rand(96) + 0.5
+    ref = R.tensor_quant(x, amax.view(1, 96), 8, False, True)
+    out = ops().fake_tensor_quant_with_axis(x.to(gpu), amax.to(gpu), 1, 8, False, True)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_int_inplace(gpu):
+    x = rand_with_edges((1000,), torch.float16, seed=4)
+    amax = torch.tensor(1.5)
+    ref = R.tensor_quant(x, amax, 8, False, True)
+    xd = x.to(gpu)
+    ops().fake_tensor_quant_(xd, amax.to(gpu), 8, False, True)
+    assert same_bits(xd, ref), mismatch(xd, ref)
+
+
+def test_int_bf16_amax_dtype(gpu):
+    # amax kept in the input dtype (MaxCalibrator output) is read directly by the kernel
+    x = rand_with_edges((128, 64), torch.bfloat16, seed=9)
+    amax = x.abs().amax(dim=1, keepdim=True)
+    ref = R.tensor_quant(x, amax, 8, False, False)
+    out = ops().quantize_op(x.to(gpu), amax.to(gpu), 8, 0, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+# --------------------------------------------------------------------------------------------
+# FP8
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_fp8_per_tensor(gpu, dtype):
+    x = rand_with_edges((257, 129), dtype, seed=1, scale=3.0)
+    amax = x.float().abs().amax() * 0.5  # clip half of the range
+    ref = R.fp8_eager(x, amax)
+    out = ops().fake_e4m3fy(x.to(gpu), amax.to(gpu))
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_fp8_special_values(gpu):
+    vals = [448.0, 449.0, 463.99, 464.0, 465.0, 480.0, 1e9, float("inf"), -float("inf"),
+            float("nan"), 0.0, -0.0, 2.0**-9, 2.0**-10, 1.5 * 2.0**-10, 2.0**-7 * 1.0625]
+    x = torch.tensor(vals, dtype=torch.float32)
+    for amax in [448.0, 0.0, 1e-30, 3.0]:
+        a = torch.tensor(amax)
+        ref = R.fp8_eager(x, a)
+        out = ops().fake_e4m3fy(x.to(gpu), a.to(gpu))
+        assert same_bits(out, ref), (amax, mismatch(out, ref))
+
+
+def test_fp8_exhaustive_bf16(gpu):
+    # every finite bf16 value through the per-tensor FP8 path at several scales
+    bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16)
+    x = bits.view(torch.bfloat16)
+    for amax in [448.0, 1.0, 3.1415, 1e-3, 6e4]:
+        a = torch.tensor(amax)
+        ref = R.fp8_eager(x, a)
+        out = ops().fake_e4m3fy(x.to(gpu), a.to(gpu))
+        assert same_bits(out, ref), (amax, mismatch(out, ref))
+
+
+def test_e4m3_cast(gpu):
+    bits = torch.arange(0, 1 << 16, dtype=torch.int32).to(torch.int16)
+    x = bits.view(torch.bfloat16)
+    ref = R.fp8_eager(x, None)
+    out = ops().e4m3_cast(x.to(gpu))
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize(
+    "shape,amax_shape", [((64, 256), (64, 1)), ((64, 256), (1, 256)), ((8192, 128), (8192, 1))]
+)
+def test_fp8_axis_and_block(gpu, dtype, shape, amax_shape):
+    x = rand_with_edges(shape, dtype, seed=21, scale=2.0)
+    g = torch.Generator().manual_seed(8)
+    amax = torch.rand(amax_shape, generator=g) * 4 + 0.01
+    amax.view(-1)[1] = 0.0
+    ref = R.fp8_eager(x, amax)
+    out = ops().quantize_op(x.to(gpu), amax.to(gpu), 8, 4, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+# --------------------------------------------------------------------------------------------
+# MX dynamic block
+# --------------------------------------------------------------------------------------------
+
+MX_FORMATS = ["E2M1", "E3M2", "E2M3", "E4M3", "E5M2", "INT8", "E1M2", "E0M3", "E3M0"]
+
+
+@pytest.mark.parametrize("fmt", MX_FORMATS)
+@pytest.mark.parametrize("bs", [8, 16, 32])
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cols", [128, 100])
+def test_mx_vs_oracle(gpu, fmt, bs, dtype, cols):
+    g = torch.Generator().manual_seed(bs + cols)
+    x = (torch.randn(33, cols, generator=g) * torch.logspace(-3, 3, cols)).to(dtype)
+    x[0, :bs] = 0.0
+    x[1, 0] = 6.0 * 2**3  # amax exactly at emax * 2^k
+    ref = R.fused_amax_convert(x, bs, fmt)
+    out = ops().fused_amax_convert(x.to(gpu), bs, R.FORMAT_CODES[fmt], R.FORMAT_CODES["E8M0"], None)
+    assert torch.equal(out.cpu().float(), ref.float()) or same_bits(out, ref), mismatch(out, ref)
+
+
+def test_mx_blocksize_error(gpu):
+    x = torch.randn(4, 64, device=gpu)
+    with pytest.raises(ValueError):
+        ops().fused_amax_convert(x, 64, R.FORMAT_CODES["E2M1"], R.FORMAT_CODES["E8M0"], None)
+
+
+# --------------------------------------------------------------------------------------------
+# amax reductions
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize(
+    "shape,axis",
+    [
+        ((1 << 20) + 7, None),
+        ((512, 4096), None),
+        ((512, 4096), 0),  # keep rows: reduce each row (weight per-channel)
+        ((512, 4096), -1),  # keep columns
+        ((4, 96, 16), 1),  # keep the middle
+        ((4, 96, 16), (0, 1)),  # keep leading run
+        ((3000, 128), 0),  # block view rows of 128
+        ((64, 3), -1),  # generic small
+        ((7, 5, 3), (1,)),
+    ],
+)
+def test_reduce_amax(gpu, dtype, shape, axis):
+    from modelopt_amd.torch.quantization.utils.core_utils import reduce_amax
+
+    shape = (shape,) if isinstance(shape, int) else shape
+    g = torch.Generator().manual_seed(len(shape))
+    x = (torch.randn(shape, generator=g) * 3).to(dtype)
+    raxis = R.convert_quantization_axis_to_reduce_axis(x, axis)
+    ref = R.reduce_amax(x, axis=raxis)
+    out = reduce_amax(x.to(gpu), axis=raxis)
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_reduce_amax_nan_inf(gpu):
+    from modelopt_amd.torch.quantization.utils.core_utils import reduce_amax
+
+    x = torch.randn(1000, 64)
+    x[10, 3] = float("nan")
+    x[20, 5] = -float("inf")
+    for axis in [None, [1], [0]]:
+        ref = R.reduce_amax(x, axis=axis)
+        out = reduce_amax(x.to(gpu), axis=axis)
+        assert same_bits(out, ref), (axis, mismatch(out, ref))
+
+
+# --------------------------------------------------------------------------------------------
+# histogram
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("bins", [2048, 3001, 20000])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_histogram_matches_histc(gpu, bins, dtype):
+    g = torch.Generator().manual_seed(bins)
+    x = (torch.randn(1 << 18, generator=g) * 2).to(dtype)
+    xa = x.float().abs()
+    hmax = xa.max()
+    ref = torch.histc(xa, bins=bins, min=0, max=float(hmax))
+    counts = torch.zeros(bins, dtype=torch.int32, device=gpu)
+    ops().histogram_abs_accumulate(x.to(gpu), hmax.to(gpu).float(), counts, bins, False)
+    assert torch.equal(counts.cpu().float(), ref), (counts.cpu().float() - ref).abs().max()
+
+
+def test_histogram_degenerate_range(gpu):
+    x = torch.zeros(1000)
+    ref = torch.histc(x, bins=64, min=0, max=0)
+    counts = torch.zeros(64, dtype=torch.int32, device=gpu)
+    ops().histogram_abs_accumulate(x.to(gpu), torch.zeros((), device=gpu), counts, 64, False)
+    assert torch.equal(counts.cpu().float(), ref)
+
+
+# --------------------------------------------------------------------------------------------
+# fused dynamic INT block quant (AWQ weight side)
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("with_pqs", [False, True])
+def test_block_quant_dynamic(gpu, dtype, with_pqs):
+    g = torch.Generator().manual_seed(1)
+    w = (torch.randn(96, 512, generator=g) * 0.02).to(dtype)
+    pqs = (torch.rand(512, generator=g) + 0.5).to(dtype) if with_pqs else None
+    ref = R.int_block_qdq_dynamic(w, 128, 4, pqs)
+    out = ops().block_quant_dynamic(w.to(gpu), None if pqs is None else pqs.to(gpu), 128, 4, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
