@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py -- MI355X fake-quant throughput (G-elem/s, % of HBM roofline) + PTQ wall-clock.
+
+Metric (BASELINE.json): "fake-quant G-elem/s (% HBM roofline) + PTQ wall-clock, Llama-3-8B FP8".
+
+A *step* is one fake-quant pass of the hot path over one batch of synthetic Llama-shaped
+activations resident in HBM: x bf16 [32768 tokens, 4096 hidden] (64 calibration samples x 512
+tokens of Llama-3-8B's hidden size) through FP8 e4m3 static block-128 quant-dequant with a
+precomputed per-block amax (the primary roofline target).  Inputs rotate over 4
+buffers (1 GiB) so the 256 MiB Infinity Cache cannot serve them.  `value` = elements processed by
+all ranks / slowest rank's time.
+
+Also reported (same JSON line):
+  roofline      dominant kernel: algorithmic bytes per launch / mean launch time (HIP events on
+                the launch stream) vs 8.0 TB/s; `traffic` from the PMC profile in profiles/ if present
+  kernels       per-kernel G-elem/s and % roofline for the other hot-path formats
+  cpu_baseline  the oracle's restatement of the reference eager path (tensor_quant.py:46-59) timed
+                on this host's cores on a bounded sample (rank 0, N=1 only)
+  ptq           Llama-3-8B FP8 PTQ wall-clock (512 synthetic samples x 512 tokens) when --ptq
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "tensorrt-model-optimizer_amd"))
+sys.path.insert(0, str(REPO))
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+TOKENS, HIDDEN, BLOCK = 32768, 4096, 128
+N_BUF = 4
+
+
+def _dist_init(n_gpus: int):
+    if n_gpus > 1 or "RANK" in os.environ:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local = int(os.environ.get("LOCAL_RANK", 0))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    return None, 0, 1
+
+
+def _barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def _max_over_ranks(dist, v: float) -> float:
+    if dist is None:
+        return v
+    t = torch.tensor([v], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_inputs(seed: int):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    xs = []
+    for i in range(N_BUF):
+        x = torch.randn(TOKENS, HIDDEN, device="cuda", dtype=torch.bfloat16, generator=g)
+        # 0.1 % outlier columns x16
+        cols = torch.randperm(HIDDEN, device="cuda", generator=g)[: HIDDEN // 1000]
+        x[:, cols] *= 16
+        xs.append(x)
+    return xs
+
+
+def time_kernel(fn, xs, steps: int, warmup: int, dist=None):
+    """Run fn over rotating inputs; returns (wall seconds for `steps`, mean event ms per launch)."""
+    outs = [None] * len(xs)
+    for i in range(warmup):
+        outs[i % len(xs)] = fn(xs[i % len(xs)])
+    torch.cuda.synchronize()
+    _barrier(dist)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        outs[i % len(xs)] = fn(xs[i % len(xs)])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    _barrier(dist)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    return wall, ms
+
+
+def kernel_suite(ops, xs, steps, warmup):
+    """Secondary per-kernel numbers (one rank)."""
+    n = xs[0].numel()
+    res = {}
+    amax_t = torch.tensor(8.0, device="cuda")
+    blk = [x.view(-1, BLOCK).abs().amax(dim=1, keepdim=True).float() for x in xs]
+    rows = [x.abs().amax(dim=1, keepdim=True).float() for x in xs]
+    cases = {
+        "fp8_per_tensor": (lambda x: ops.fake_e4m3fy(x, amax_t), 4),
+        "int8_per_tensor": (lambda x: ops.fake_tensor_quant(x, amax_t, 8, False, False), 4),
+        "int8_per_channel_axis0": (
+            lambda x: ops.quantize_op(x, rows[[id(t) for t in xs].index(id(x))], 8, 0, False, False), 4),
+        "int4_block128_static": (
+            lambda x: ops.quantize_op(x.view(-1, BLOCK), blk[[id(t) for t in xs].index(id(x))], 4, 0, False, False), 4),
+        "mxfp4_block32_dynamic": (lambda x: ops.fused_amax_convert(x, 32, 6, 9, None), 4),
+        "mxfp8_block32_dynamic": (lambda x: ops.fused_amax_convert(x, 32, 0, 9, None), 4),
+        "int4_block128_dynamic_awq": (lambda x: ops.block_quant_dynamic(x, None, 128, 4, False, False), 4),
+        "amax_per_tensor": (None, 2),
+    }
+    acc = torch.zeros(1, device="cuda")
+    for name, (fn, bpe) in cases.items():
+        if fn is None:
+            def fn(x):  # noqa: E306
+                ops.amax_accumulate(x, acc, 1, 1, x.numel())
+                return acc
+        _, ms = time_kernel(fn, xs, max(steps, 10), warmup)
+        gbs = n * bpe / (ms * 1e-3) / 1e9
+        res[name] = {
+            "gelem_s": round(n / (ms * 1e-3) / 1e9, 1),
+            "GB_s": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "ms": round(ms, 4),
+        }
+    return res
+
+
+def cpu_baseline(target_s: float = 10.0):
+    """Oracle restatement of the reference eager FP8 block path, timed on host cores."""
+    from oracle import ref_ops as R  # test infrastructure: the checker / CPU baseline only
+
+    rows = 8192  # bounded sample: [8192, 4096] bf16 = 33.5 M elements per pass
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(rows, HIDDEN, generator=g).to(torch.bfloat16)
+    xb = x.view(-1, BLOCK)
+    amax = xb.abs().amax(dim=1, keepdim=True).float()
+    R.fp8_eager(xb, amax)  # warm-up
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        R.fp8_eager(xb, amax)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= target_s or passes >= 200:
+            break
+    elems = passes * x.numel()
+    return {
+        "value": round(elems / el / 1e9, 4),
+        "unit": "G-elem/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"{passes} passes of FP8 e4m3 static block-128 fake-quant (oracle fp8_eager, the "
+        f"reference _fp8_eager ATen sequence) over bf16 [{rows}, {HIDDEN}], {el:.1f} s",
+    }
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed PMC profile, if any."""
+    for p in sorted((REPO / "profiles").glob("traffic_*.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())
+            if d.get("kernel_config") == f"fp8_block{BLOCK}_bf16_{TOKENS}x{HIDDEN}":
+                return d.get("hbm_bytes_per_launch"), p.name
+        except Exception:  # noqa: BLE001
+            continue
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-suite", action="store_true", help="skip the secondary kernel table")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--ptq", action="store_true", help="also time Llama-3-8B FP8 PTQ (512 samples)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    dist, rank, world = _dist_init(args.gpus)
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    xs = make_inputs(1234 + rank)
+    blk = [x.view(-1, BLOCK).abs().amax(dim=1, keepdim=True).float() for x in xs]
+    idx = {id(x): i for i, x in enumerate(xs)}
+
+    def step(x):
+        return ops.quantize_op(x.view(-1, BLOCK), blk[idx[id(x)]], 8, 4, False, False)
+
+    wall, ms = time_kernel(step, xs, args.steps, args.warmup, dist)
+    wall = _max_over_ranks(dist, wall)
+    n = xs[0].numel()
+    total = n * args.steps * world
+    value = total / wall / 1e9
+    alg_bytes = n * 4 + (n // BLOCK) * 4  # read x bf16 + write y bf16 + read fp32 amax
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic()
+
+    out = {
+        "metric": "fake-quant G-elem/s (% HBM roofline) + PTQ wall-clock, Llama-3-8B FP8",
+        "value": round(value, 2),
+        "unit": "G-elem/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (seeded randn bf16, 0.1% outlier columns x16; amax precomputed per block)",
+        "config": {
+            "workload": "FP8 e4m3 static block-128 fake quant-dequant of Llama-3-8B activations "
+            f"[{TOKENS} tokens x {HIDDEN}] bf16 per rank (SURVEY K3)",
+            "tokens_per_rank": TOKENS,
+            "hidden": HIDDEN,
+            "block": BLOCK,
+            "parallelism": f"dp{world} (independent shards, no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": "mtq fp8 axis (Fp8AxisVecOp<bf16>) via modelopt_amd::quantize_op",
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "mean_launch_ms": round(ms, 4),
+        },
+    }
+    if rank == 0 and not args.no_suite:
+        out["kernels"] = kernel_suite(ops, xs, args.steps, args.warmup)
+    if rank == 0 and args.ptq:
+        from scripts import ptq_llama  # noqa: PLC0415
+
+        out["ptq"] = ptq_llama.run(samples=512, seq=512)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -68,6 +68,20 @@ template <typename T>
 __device__ __forceinline__ void stg_vec(T *p, const Vec<T> &v) {
   *reinterpret_cast<uint4 *>(p) = v.raw;
 }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// streaming (non-temporal) forms: the data is touched exactly once
+template <typename T>
+__device__ __forceinline__ Vec<T> ldg_vec_nt(const T *p) {
+  u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+  Vec<T> v;
+  v.raw = make_uint4(r.x, r.y, r.z, r.w);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ void stg_vec_nt(T *p, const Vec<T> &v) {
+  u32x4 r = {v.raw.x, v.raw.y, v.raw.z, v.raw.w};
+  __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(p));
+}
 
 // amax pointer of any dtype -> fp32 (reference: amax.to(at::ScalarType::Float)).
 __device__ __forceinline__ float load_as_float(const void *p, int dtype, int64_t i) {

@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "mtq_amd.h"
 #include "mtq_device.hpp"
@@ -20,7 +21,6 @@ using namespace mtq;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 4;
 
 thread_local int g_last_hip_error = 0;
 
@@ -73,28 +73,43 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 //   vec(Vec<T>&, int64_t vi)     quantise one 16-byte vector (vector index vi)
 //   one(float x, int64_t i)      quantise one element (element index i)
 // ============================================================================================
-template <typename T, class Op>
+// Launch structure (measured with scripts/bw_probe.hip on MI355X, bf16 256 MiB in + out):
+// one 16-byte vector per lane, each block a contiguous chunk of 256*U vectors, one chunk per
+// block (no grid-stride loop), reaches 6.1 TB/s; a grid-stride loop with 4 vectors in flight per
+// lane over 2048 blocks only 4.3-4.6 TB/s.  `variant` selects U / non-temporal for tuning.
+template <typename T, class Op, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void ew_vec_kernel(const T *__restrict__ x,
                                                            T *__restrict__ y, int64_t nvec,
                                                            Op op) {
   using V = Vec<T>;
   op.init();
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
-    V v[kUnroll];
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  V v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = ldg_vec(x + (i + u * stride) * V::N);
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) op.vec(v[u], i + u * stride);
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) stg_vec(y + (i + u * stride) * V::N, v[u]);
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i < nvec) v[u] = NT ? ldg_vec_nt(x + i * V::N) : ldg_vec(x + i * V::N);
   }
-  for (; i < nvec; i += stride) {
-    V v = ldg_vec(x + i * V::N);
-    op.vec(v, i);
-    stg_vec(y + i * V::N, v);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i < nvec) {
+      op.vec(v[u], i);
+      if (NT)
+        stg_vec_nt(y + i * V::N, v[u]);
+      else
+        stg_vec(y + i * V::N, v[u]);
+    }
   }
+}
+
+int ew_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("MTQ_AMD_EW_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
 }
 
 template <typename T, class Op>
@@ -115,8 +130,16 @@ int launch_ew(const void *xv, void *yv, int64_t n, Op op, hipStream_t stream) {
   constexpr int N = Vec<T>::N;
   int64_t nvec = (aligned16(x) && aligned16(y)) ? n / N : 0;
   if (nvec > 0) {
-    unsigned g = grid_for(nvec, kThreads * kUnroll);
-    ew_vec_kernel<T, Op><<<g, kThreads, 0, stream>>>(x, y, nvec, op);
+    auto blocks = [&](int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); };
+    // variant 0 (default): U = 1, non-temporal -- best of the r01 sweep (scripts/sweep_ew.py:
+    // fp8 per-tensor 6.28 TB/s, fp8 block-128 6.0 TB/s vs 5.9 / 5.87 for U = 1 temporal)
+    switch (ew_variant()) {
+    case 1: ew_vec_kernel<T, Op, 2, false><<<blocks(2), kThreads, 0, stream>>>(x, y, nvec, op); break;
+    case 2: ew_vec_kernel<T, Op, 1, false><<<blocks(1), kThreads, 0, stream>>>(x, y, nvec, op); break;
+    case 3: ew_vec_kernel<T, Op, 2, true><<<blocks(2), kThreads, 0, stream>>>(x, y, nvec, op); break;
+    case 4: ew_vec_kernel<T, Op, 4, true><<<blocks(4), kThreads, 0, stream>>>(x, y, nvec, op); break;
+    default: ew_vec_kernel<T, Op, 1, true><<<blocks(1), kThreads, 0, stream>>>(x, y, nvec, op); break;
+    }
   }
   int64_t done = nvec * N;
   if (done < n) {
@@ -379,29 +402,22 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   constexpr int N = V::N;
   constexpr int LPB = BS / N >= 1 ? BS / N : 1;
   static_assert(BS % N == 0, "block must be a multiple of the vector");
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  // stride and the start index are multiples of LPB, so the LPB lanes of a block stay together
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i - (threadIdx.x % LPB) < nvec;
-       i += stride) {
-    const bool live = i < nvec;
-    V v;
-    if (live) v = ldg_vec(x + i * N);
-    float m = 0.f;
-    if (live) {
+  // nvec % LPB == 0 and kThreads % LPB == 0: the LPB lanes of an MX block are all live or all out
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i - (threadIdx.x % LPB) >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  float m = 0.f;
 #pragma unroll
-      for (int j = 0; j < N; ++j) m = fmaxf(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
-    }
-    m = group_max_f<LPB>(m);
-    if (!live) continue;
-    const int64_t blk = i / LPB;
-    const int64_t row = (blk * BS) / p.cols;
-    float scale, unscale;
-    mx_block_scale(m, row, p, scale, unscale);
+  for (int j = 0; j < N; ++j) m = fmaxf(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
+  m = group_max_f<LPB>(m);
+  const int64_t blk = i / LPB;
+  const int64_t row = (blk * BS) / p.cols;
+  float scale, unscale;
+  mx_block_scale(m, row, p, scale, unscale);
 #pragma unroll
-    for (int j = 0; j < N; ++j)
-      v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, p.fmt));
-    stg_vec(y + i * N, v);
-  }
+  for (int j = 0; j < N; ++j)
+    v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, p.fmt));
+  stg_vec_nt(y + i * N, v);
 }
 
 // General path: one lane per element of the zero-padded [rows, padded_cols] matrix; BS lanes
@@ -438,7 +454,7 @@ int launch_mx(const void *xv, void *yv, int64_t rows, int64_t cols, int bs, MxPa
   const int64_t n = rows * cols;
   if (cols % bs == 0 && bs % N == 0 && aligned16(x) && aligned16(y)) {
     int64_t nvec = n / N;
-    unsigned g = grid_for(nvec, kThreads);
+    unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
     switch (bs) {
     case 8: mx_vec_kernel<T, 8><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
     case 16: mx_vec_kernel<T, 16><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
@@ -481,18 +497,7 @@ __global__ __launch_bounds__(kThreads) void amax_all_kernel(const T *__restrict_
   __shared__ uint32_t red[kThreads / 64];
   uint32_t m = 0;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
-  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < nvec; i += kUnroll * stride) {
-    V v[kUnroll];
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = ldg_vec(x + (i + u * stride) * V::N);
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      uint32_t b = vec_absmax_bits(v[u]);
-      m = b > m ? b : m;
-    }
-  }
-  for (; i < nvec; i += stride) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride) {
     uint32_t b = vec_absmax_bits(ldg_vec(x + i * V::N));
     m = b > m ? b : m;
   }
@@ -597,7 +602,7 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
   const bool al = aligned16(x);
   if (K == 1 && (Q == 1 || P == 1)) {  // per-tensor
     int64_t nvec = al ? n / N : 0;
-    unsigned g = grid_for(n / N + 1, kThreads * kUnroll * 4);
+    unsigned g = grid_for(n / N + 1, kThreads * 4);
     amax_all_kernel<T><<<g, kThreads, 0, stream>>>(x, n, nvec, out);
     return check_launch();
   }
@@ -654,30 +659,20 @@ __global__ __launch_bounds__(kThreads) void block_quant_dyn_kernel(
   using V = Vec<T>;
   constexpr int N = V::N;
   constexpr int LPB = BLK / N;
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i - (threadIdx.x % LPB) < nvec;
-       i += stride) {
-    const bool live = i < nvec;
-    V v;
-    uint32_t m = 0;
-    if (live) {
-      v = ldg_vec(x + i * N);
-      if (pqs) {
-        const int64_t col = (i * N) % cols;
-        V s = ldg_vec(pqs + col);
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i - (threadIdx.x % LPB) >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  if (pqs) {
+    const int64_t col = (i * N) % cols;
+    V s = ldg_vec(pqs + col);
 #pragma unroll
-        for (int j = 0; j < N; ++j)
-          v.e[j] = Elem<T>::st(Elem<T>::ld(v.e[j]) * Elem<T>::ld(s.e[j]));
-      }
-      m = vec_absmax_bits(v);
-    }
-    m = group_max_u32<LPB>(m);
-    if (!live) continue;
-    IntQ q = make_intq(__uint_as_float(m), max_bound, min_bound);
-#pragma unroll
-    for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
-    stg_vec(y + i * N, v);
+    for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(Elem<T>::ld(v.e[j]) * Elem<T>::ld(s.e[j]));
   }
+  uint32_t m = group_max_u32<LPB>(vec_absmax_bits(v));
+  IntQ q = make_intq(__uint_as_float(m), max_bound, min_bound);
+#pragma unroll
+  for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
+  stg_vec_nt(y + i * N, v);
 }
 
 // ============================================================================================
@@ -883,7 +878,7 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
         (pqs && !aligned16(pqs)))
       return MTQ_ERR_INVALID_ARG;
     const int64_t nvec = rows * cols / N;
-    unsigned g = grid_for(nvec, kThreads);
+    unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
     const T *xt = reinterpret_cast<const T *>(x);
     T *yt = reinterpret_cast<T *>(y);
     const T *pt = reinterpret_cast<const T *>(pqs);
