@@ -212,17 +212,13 @@ def compute_amax_entropy(calib_hist, calib_bin_edges, num_bits, unsigned, stride
             if digitized != -1:
                 new_density[idx] = new_density_counts[digitized]
         total_counts_new = np.sum(new_density) + np.sum(bins[i:])
-        s = np.sum(new_density)
-        if s != 0:
-            new_density = new_density / s
+        # the reference's _normalize_distr rebinds its local and is a no-op (histogram.py:216-219);
+        # scipy's entropy normalises both densities itself
         reference_density = np.array(bins[: len(digitized_space)])
         reference_density[-1] += np.sum(bins[i:])
         total_counts_old = np.sum(reference_density)
         if round(total_counts_new) != total_data or round(total_counts_old) != total_data:
             raise RuntimeError("Count mismatch!")
-        s = np.sum(reference_density)
-        if s != 0:
-            reference_density = reference_density / s
         divergences.append(entropy(reference_density, new_density))
     divergences = np.array(divergences)
     last_argmin = len(divergences) - 1 - np.argmin(divergences[::-1])

@@ -58,31 +58,54 @@ int checked_dtype(const at::Tensor &t, const char *name) {
 // a run such as amax [B, T, 1] on input [B, T, H] merges into one axis).
 struct AxisMap {
   bool per_tensor;
+  bool adjacent;  // false: the quantized axes are not one contiguous run (see permuted())
   int64_t axis_size, inner;
 };
 
 AxisMap axis_map(const at::Tensor &x, const at::Tensor &amax) {
-  if (amax.numel() == 1) return {true, 1, 1};
+  if (amax.numel() == 1) return {true, true, 1, 1};
   const int64_t xd = x.dim(), ad = amax.dim();
   TORCH_CHECK(ad <= xd, "modelopt_amd: amax of rank ", ad, " does not broadcast to input of rank ",
               xd);
   int first = -1, last = -1;
+  bool adjacent = true;
   for (int64_t i = 0; i < ad; ++i) {
     const int64_t xi = xd - ad + i;
     if (amax.size(i) != 1) {
       TORCH_CHECK(amax.size(i) == x.size(xi), "modelopt_amd: amax shape ", amax.sizes(),
                   " does not broadcast to input shape ", x.sizes());
       if (first < 0) first = (int)xi;
-      TORCH_CHECK(last < 0 || last == xi - 1,
-                  "modelopt_amd: amax with non-adjacent quantization axes is not supported (shape ",
-                  amax.sizes(), ")");
+      if (last >= 0 && last != xi - 1) adjacent = false;
       last = (int)xi;
     }
   }
+  if (!adjacent) return {false, false, 0, 0};
   int64_t axis_size = 1, inner = 1;
   for (int i = first; i <= last; ++i) axis_size *= x.size(i);
   for (int64_t i = last + 1; i < xd; ++i) inner *= x.size(i);
-  return {false, axis_size, inner};
+  return {false, true, axis_size, inner};
+}
+
+// Non-adjacent quantization axes (e.g. the 2-D block view [2, 2, 3, 2, 2] with amax
+// [2, 2, 1, 2, 1], tensor_quantizer_common.py:501-516): move the quantized axes to the front
+// (device permute copies), quantize with one merged axis, and permute back.
+template <class Fn>
+at::Tensor permuted(const at::Tensor &x, const at::Tensor &amax, Fn fn) {
+  const int64_t xd = x.dim();
+  at::Tensor a = amax.reshape([&] {
+    std::vector<int64_t> s(xd - amax.dim(), 1);
+    for (auto v : amax.sizes()) s.push_back(v);
+    return s;
+  }());
+  std::vector<int64_t> perm, rest;
+  for (int64_t i = 0; i < xd; ++i) (a.size(i) != 1 ? perm : rest).push_back(i);
+  perm.insert(perm.end(), rest.begin(), rest.end());
+  std::vector<int64_t> inv(xd);
+  for (int64_t i = 0; i < xd; ++i) inv[perm[i]] = i;
+  at::Tensor xp = x.permute(perm).contiguous();
+  at::Tensor ap = a.permute(perm).contiguous();
+  at::Tensor yp = fn(xp, ap);
+  return yp.permute(inv).contiguous();
 }
 
 at::Tensor amax_operand(const at::Tensor &amax, const at::Tensor &x) {
@@ -95,11 +118,21 @@ at::Tensor amax_operand(const at::Tensor &amax, const at::Tensor &x) {
 
 // ---- INT ---------------------------------------------------------------------------------------
 void int_qdq_into(const at::Tensor &x, at::Tensor &y, const at::Tensor &amax_in, int64_t num_bits,
+                  bool is_unsigned, bool narrow_range);
+void int_qdq_into(const at::Tensor &x, at::Tensor &y, const at::Tensor &amax_in, int64_t num_bits,
                   bool is_unsigned, bool narrow_range) {
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
   at::Tensor amax = amax_operand(amax_in, x);
   AxisMap m = axis_map(x, amax);
+  if (!m.adjacent) {
+    y.copy_(permuted(x, amax, [&](const at::Tensor &xp, const at::Tensor &ap) {
+      at::Tensor yp = at::empty_like(xp);
+      int_qdq_into(xp, yp, ap, num_bits, is_unsigned, narrow_range);
+      return yp;
+    }));
+    return;
+  }
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   int st;
   if (m.per_tensor)
@@ -150,12 +183,16 @@ at::Tensor fake_tensor_quant_with_axis(const at::Tensor &inputs, const at::Tenso
 }
 
 // ---- FP8 -----------------------------------------------------------------------------------
+at::Tensor fp8_qdq(const at::Tensor &inputs, const at::Tensor &amax_in);
 at::Tensor fp8_qdq(const at::Tensor &inputs, const at::Tensor &amax_in) {
   at::Tensor x = inputs.contiguous();
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
   at::Tensor amax = amax_operand(amax_in, x);
   AxisMap m = axis_map(x, amax);
+  if (!m.adjacent) return permuted(x, amax, [](const at::Tensor &xp, const at::Tensor &ap) {
+    return fp8_qdq(xp, ap);
+  });
   at::Tensor y = at::empty_like(x);
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   int st;

@@ -1,0 +1,215 @@
+"""Histogram calibrator on the LDS-privatised |x| histogram kernel.
+
+Reference: modelopt/torch/quantization/calib/histogram.py:35-343.  ``collect`` keeps the
+reference's torch-histogram branch semantics exactly (``torch.histc(|x|, bins, 0, max)`` with the
+first-call ``linspace`` edges and the fixed-width bin growth of :108-130); the histogram itself is
+one launch of ``histogram_abs_accumulate`` plus one of the max|x| reduction (the reference: abs,
+float copy, max, histc -- and a ``torch.min(x) < 0`` host sync).  Counts are exact integers per
+call (the reference accumulates float counts, which stop at 2^24 per bin).
+``compute_amax`` runs on the host like the reference (entropy / MSE / percentile); the MSE sweep
+quantises the bin centres with the HIP kernels.
+"""
+
+from __future__ import annotations
+
+import warnings
+from collections import Counter
+
+import numpy as np
+import torch
+
+from modelopt_amd._ext import ops as _ops
+
+from ..tensor_quant import fake_tensor_quant, fp8_fake_quant
+from ..utils import core_utils as quant_utils
+from .calibrator import _Calibrator
+
+__all__ = ["HistogramCalibrator"]
+
+
+class HistogramCalibrator(_Calibrator):
+    def __init__(
+        self,
+        num_bits=8,
+        axis=None,
+        unsigned=False,
+        num_bins=2048,
+        grow_method=None,
+        skip_zeros=False,
+        torch_hist=True,
+    ):
+        super().__init__(num_bits, axis, unsigned)
+        self._num_bins = num_bins
+        self._skip_zeros = skip_zeros
+        self._calib_bin_edges = None
+        self._calib_hist = None
+        self._torch_hist = torch_hist
+        if axis is not None:
+            raise NotImplementedError("Calibrator histogram collection only supports per tensor scaling")
+        if not torch_hist:
+            raise NotImplementedError(
+                "modelopt_amd: the numpy (host) histogram branch is not part of the MI355X path; "
+                "use torch_hist=True"
+            )
+
+    @torch.no_grad()
+    def collect(self, x):
+        # max|x| (equals the reference's max over the non-zero |x| when skip_zeros, histogram.py:105-112)
+        x_max = torch.zeros((), dtype=torch.float32, device=x.device)
+        quant_utils.reduce_amax_accumulate(x, x_max, None)
+        if self._calib_bin_edges is None and self._calib_hist is None:
+            hmax = x_max
+            bins = self._num_bins
+            self._calib_bin_edges = torch.linspace(0, float(x_max), self._num_bins + 1)
+            old = None
+        else:
+            xm = x_max.cpu()
+            if float(xm) > float(self._calib_bin_edges[-1]):
+                width = (self._calib_bin_edges[1] - self._calib_bin_edges[0]).cpu()
+                self._num_bins = int((xm / width).ceil().item())
+                # the edges are host bookkeeping: built with the CPU arange (double accumulation),
+                # the reference-CPU semantics; a device arange rounds the edges differently
+                self._calib_bin_edges = torch.arange(0, xm + width, width)
+            bins = self._num_bins
+            hmax = self._calib_bin_edges[-1].to(device=x.device, dtype=torch.float32).reshape(())
+            old = self._calib_hist
+        counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
+        _ops().histogram_abs_accumulate(x, hmax.float().contiguous(), counts, bins, self._skip_zeros)
+        hist = counts.float()
+        if old is not None:
+            hist[: old.numel()] += old.to(hist.device)
+        self._calib_hist = hist
+
+    def reset(self):
+        self._calib_bin_edges = None
+        self._calib_hist = None
+
+    def compute_amax(self, method: str, *, stride: int = 1, start_bin: int = 128, percentile: float = 99.99):
+        import torch.distributed as tdist
+
+        if tdist.is_available() and tdist.is_initialized():
+            warnings.warn(
+                "This method does not perform any synchronization across distributed processes. The "
+                "recommended method is to use the same calibration dataset across all distributed data "
+                "parallel groups so that `amax` is the same for all DDP modules."
+            )
+        if self._calib_hist is None:
+            return None
+        calib_hist = self._calib_hist.int().cpu().numpy()
+        calib_bin_edges = self._calib_bin_edges.cpu().numpy()
+        if method == "entropy":
+            return _compute_amax_entropy(
+                calib_hist, calib_bin_edges, self._num_bits, self._unsigned, stride, start_bin
+            )
+        if method == "mse":
+            return _compute_amax_mse(
+                calib_hist, calib_bin_edges, self._num_bits, self._unsigned, stride, start_bin,
+                device=self._calib_hist.device,
+            )
+        if method == "percentile":
+            return _compute_amax_percentile(calib_hist, calib_bin_edges, percentile)
+        raise TypeError(f"Unknown calibration method {method}")
+
+    def __str__(self):
+        if self._calib_bin_edges is None:
+            e = "None"
+        else:
+            e = f"[{float(self._calib_bin_edges[0]):.3f}, ..., {float(self._calib_bin_edges[-1]):.3f}]({len(self._calib_bin_edges)})"
+        return f"HistogramCalibrator(calib_bin_edges={e})"
+
+
+def _compute_amax_entropy(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128):
+    """KL-divergence amax (histogram.py:210-282).
+
+    Same arithmetic as the reference loop, with the per-candidate Python loops replaced by numpy
+    gathers/bincounts: for candidate i the quantised density assigns every non-empty bin j < i the
+    mean count of the non-empty bins in its quantisation level (np.digitize over linspace(0, i)).
+    """
+    from scipy.stats import entropy
+
+    if calib_bin_edges is None and calib_hist is None:
+        return None
+    bins = calib_hist[:]
+    bins[0] = bins[1]
+    total_data = np.sum(bins)
+    divergences = []
+    nbins = 1 << (num_bits - 1 + int(unsigned))
+    for i in range(start_bin, len(bins) + 1, stride):
+        space = np.linspace(0, i, num=nbins + 1)
+        digitized = np.digitize(range(i), space) - 1
+        digitized[bins[:i] == 0] = -1
+        valid = digitized != -1
+        dv = digitized[valid]
+        level_sum = np.zeros(nbins, dtype=np.float64)
+        # sequential accumulation order matters for float64 sums of integers < 2^53: exact anyway
+        np.add.at(level_sum, dv, bins[:i][valid].astype(np.float64))
+        level_cnt = np.bincount(dv, minlength=nbins)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            level_mean = np.where(level_cnt > 0, level_sum / np.maximum(level_cnt, 1), 0.0)
+        new_density = np.zeros(i, dtype=np.float64)
+        new_density[valid] = level_mean[dv]
+        total_counts_new = np.sum(new_density) + np.sum(bins[i:])
+        # the reference's _normalize_distr rebinds its local and is a no-op (histogram.py:216-219);
+        # scipy's entropy normalises both densities itself
+        reference_density = np.array(bins[: len(digitized)])
+        reference_density[-1] += np.sum(bins[i:])
+        total_counts_old = np.sum(reference_density)
+        if round(total_counts_new) != total_data or round(total_counts_old) != total_data:
+            raise RuntimeError(
+                f"Count mismatch! total_counts_new={total_counts_new}, "
+                f"total_counts_old={total_counts_old}, total_data={total_data}"
+            )
+        divergences.append(entropy(reference_density, new_density))
+    divergences = np.array(divergences)
+    last_argmin = len(divergences) - 1 - np.argmin(divergences[::-1])
+    return torch.tensor(calib_bin_edges[last_argmin * stride + start_bin].item())
+
+
+def _compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128,
+                      device=None):
+    """MSE amax (histogram.py:285-325): every candidate quantises the bin centres on the GPU; the
+    per-candidate MSEs are gathered once instead of one host sync per candidate.
+
+    Divergence: the reference calls ``fake_tensor_quant(centers, amax, num_bits, unsigned)``, which
+    binds ``num_bits`` to the functional's ``bias`` slot (tensor_quant.py:337-349), and
+    ``scaled_e4m3(centers, amax, 4, 3)`` (missing M).  Here the candidates are quantised with the
+    documented intent (``num_bits``-bit, narrow range, no bias); MSE amax parity is therefore
+    against that intent, not against the reference's outputs.
+    """
+    if calib_bin_edges is None and calib_hist is None:
+        return None
+    counts = torch.from_numpy(calib_hist[:]).float()
+    edges = torch.from_numpy(calib_bin_edges[:]).float()
+    if device is not None and device.type == "cuda":
+        counts = counts.to(device)
+        edges = edges.to(device)
+    centers = (edges[1:] + edges[:-1]) / 2
+    mses, arguments = [], []
+    for i in range(start_bin, len(centers), stride):
+        amax = centers[i]
+        if isinstance(num_bits, int) and num_bits >= 0:
+            quant_centers = fake_tensor_quant(centers, amax, None, num_bits, unsigned)
+        elif num_bits == (4, 3):
+            quant_centers = fp8_fake_quant(centers, amax)
+        else:
+            raise TypeError("Invalid num_bits. num_bits must be a positive integer or tuple (4,3).")
+        mses.append(((quant_centers - centers) ** 2 * counts).mean())
+        arguments.append(i)
+    mses_np = torch.stack(mses).cpu().numpy()
+    argmin = np.argmin(mses_np)
+    return centers[arguments[argmin]]
+
+
+def _compute_amax_percentile(calib_hist, calib_bin_edges, percentile):
+    """Percentile amax (histogram.py:328-343)."""
+    if percentile < 0 or percentile > 100:
+        raise ValueError("Invalid percentile. Must be in range 0 <= percentile <= 100.")
+    if calib_bin_edges is None and calib_hist is None:
+        return None
+    total = calib_hist.sum()
+    cdf = np.cumsum(calib_hist / total)
+    idx = np.searchsorted(cdf, percentile / 100)
+    return torch.tensor(calib_bin_edges[idx].item())
+
+
+_ = Counter  # kept for parity with the reference module's imports

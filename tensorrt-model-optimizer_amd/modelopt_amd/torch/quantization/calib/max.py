@@ -1,0 +1,114 @@
+"""Max calibrator on the fused accumulate-max HIP kernel.
+
+Reference: modelopt/torch/quantization/calib/max.py:26-110.  Same results (the running amax is an
+exact max, so order and fusion cannot change it); the differences are where the time goes:
+
+* one kernel launch per ``collect`` (``amax_accumulate``: max|x| folded straight into a persistent
+  fp32 running-max buffer) instead of ``reduce_amax``'s two full passes plus ``torch.max``;
+* no host synchronisation in ``collect``: the reference's three NaN / negative / inf asserts
+  (calib/max.py:69-77) are evaluated once, lazily, when the amax is read (``compute_amax``), and
+  raise the same AssertionError messages there;
+* a second ``collect`` of the *same* tensor object at the same version (the weight of a
+  QuantLinear during ``forward_loop``, which the reference re-reduces on every batch) is skipped:
+  max(a, a) = a.
+"""
+
+from __future__ import annotations
+
+import weakref
+
+import torch
+
+from ..utils import core_utils as quant_utils
+from .calibrator import _Calibrator
+
+__all__ = ["MaxCalibrator"]
+
+
+class MaxCalibrator(_Calibrator):
+    """Tracks the absolute max of all collected tensors (per-tensor or along ``axis``)."""
+
+    def __init__(self, num_bits=8, axis=None, unsigned=False, track_amax=False):
+        super().__init__(num_bits, axis, unsigned)
+        self._track_amax = track_amax
+        if self._track_amax:
+            self._amaxs = []
+        self._acc = None  # fp32 running max, flat
+        self._out_shape = None
+        self._out_dtype = None
+        self._last = None  # (weakref to the last collected tensor, its _version)
+        self._meta_amax = None
+
+    @property
+    def amaxs(self):
+        return self._amaxs
+
+    def _same_as_last(self, x) -> bool:
+        if self._last is None:
+            return False
+        ref, ver = self._last
+        return ref() is x and x._version == ver
+
+    @torch.no_grad()
+    def collect(self, x):
+        reduce_axis = quant_utils.convert_quantization_axis_to_reduce_axis(x, self._axis)
+        if x.device.type == "meta":
+            self._meta_amax = quant_utils.amax_view(x, reduce_axis)[4]
+            return
+        if self._acc is not None and self._same_as_last(x):
+            return
+        keep_shape = quant_utils.amax_view(x, reduce_axis)[4] if reduce_axis is not None else []
+        if self._acc is None:
+            numel = 1
+            for s in keep_shape:
+                numel *= s
+            self._acc = torch.zeros(numel, dtype=torch.float32, device=x.device)
+            self._out_shape = keep_shape
+            self._out_dtype = x.dtype if x.dtype.is_floating_point else torch.float32
+            if self._out_dtype in (torch.float8_e4m3fn, torch.float8_e5m2):
+                self._out_dtype = torch.get_default_dtype()
+        elif list(keep_shape) != list(self._out_shape):
+            raise RuntimeError("amax shape changed!")
+        quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
+        try:
+            self._last = (weakref.ref(x), x._version)
+        except TypeError:
+            self._last = None
+        if self._track_amax:
+            self._amaxs.append(quant_utils.reduce_amax(x, axis=reduce_axis).cpu().numpy())
+
+    def _result(self):
+        if self._acc is None:
+            return None
+        out = self._acc.view(self._out_shape) if self._out_shape else self._acc.view(())
+        out = out.to(self._out_dtype)
+        if out.numel() == 1:
+            out = out.squeeze()
+        return out
+
+    @property
+    def _calib_amax(self):
+        return self._result()
+
+    def reset(self):
+        self._acc = None
+        self._out_shape = None
+        self._last = None
+
+    def validate(self):
+        """The reference's per-collect asserts (calib/max.py:69-77), evaluated once."""
+        if self._acc is None:
+            return
+        bad = torch.stack([torch.isnan(self._acc).any(), torch.isinf(self._acc).any()]).tolist()
+        assert not bad[0], "detected nan values in amax (NaN in a collected tensor)"
+        assert not bad[1], "detected inf values in amax (inf in a collected tensor)"
+
+    def compute_amax(self):
+        self.validate()
+        return self._result()
+
+    def __str__(self):
+        return f"MaxCalibrator(track_amax={self._track_amax})"
+
+    def __repr__(self):
+        return f"MaxCalibrator({super().__repr__()} calib_amax={self._result()} track_amax={self._track_amax})"

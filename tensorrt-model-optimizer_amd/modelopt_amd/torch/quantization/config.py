@@ -1,0 +1,526 @@
+"""Quantizer attribute / quantize configs and the preset configs of the hot path.
+
+Mirrors the schema of modelopt/torch/quantization/config.py: ``QuantizerAttributeConfig``
+(:322-709), ``QuantizerCfgEntry`` (:165-243) with its normalisation rules, ``QuantizeConfig``
+(:1573), the calibration-algorithm configs used on the PTQ path (``MaxCalibConfig`` :894,
+``AWQLiteCalibConfig`` :1084), and the preset dicts (``INT8_DEFAULT_CFG`` ... :1681-1778) that the
+reference composes from ``modelopt_recipes/configs/ptq/...`` YAML units.  The presets here are
+written out as plain dicts with the same entries (no YAML loader on the hot path).
+"""
+
+from __future__ import annotations
+
+import copy
+import re
+from collections.abc import Callable, Mapping
+from typing import Any
+
+from pydantic import BaseModel, ConfigDict, Field, ValidationInfo, field_validator, model_validator
+
+__all__ = [
+    "AWQClipCalibConfig",
+    "AWQFullCalibConfig",
+    "AWQLiteCalibConfig",
+    "MaxCalibConfig",
+    "QuantizeAlgorithmConfig",
+    "QuantizeConfig",
+    "QuantizerAttributeConfig",
+    "QuantizerCfgEntry",
+    "choices",
+    "need_calibration",
+    "normalize_quant_cfg_list",
+]
+
+
+class _Config(BaseModel):
+    """Pydantic base with the dict-like accessors the reference's ModeloptBaseConfig offers."""
+
+    model_config = ConfigDict(extra="forbid", validate_assignment=True, arbitrary_types_allowed=True)
+
+    def items(self):
+        return self.model_dump().items()
+
+    def keys(self):
+        return self.model_dump().keys()
+
+    def get(self, key, default=None):
+        return getattr(self, key, default)
+
+    def __getitem__(self, key):
+        return getattr(self, key)
+
+    def __contains__(self, key):
+        return key in type(self).model_fields
+
+
+_EXMY = re.compile(r"^e(\d+)m(\d+)$", re.IGNORECASE)
+_FP_FORMATS = [(4, 3), (5, 2), (2, 1), (1, 2), (0, 3), (3, 0), (3, 2), (2, 3)]
+
+
+def _parse_num_bits(v):
+    if isinstance(v, str):
+        m = _EXMY.match(v.strip())
+        if m:
+            return (int(m.group(1)), int(m.group(2)))
+        if v.isdigit():
+            return int(v)
+        return v
+    if isinstance(v, list):
+        return tuple(v)
+    return v
+
+
+def _parse_block_sizes(v):
+    if v is None:
+        return None
+    out = {}
+    for k, val in dict(v).items():
+        if isinstance(k, str) and k.lstrip("-").isdigit():
+            k = int(k)
+        if k == "scale_bits" and isinstance(val, (list, str)):
+            val = _parse_num_bits(val)
+        if k == "scale_block_sizes" and isinstance(val, Mapping):
+            val = {int(a) if isinstance(a, str) and a.lstrip("-").isdigit() else a: b for a, b in val.items()}
+        out[k] = val
+    return out
+
+
+class QuantizerAttributeConfig(_Config):
+    """Attributes of one TensorQuantizer (reference config.py:322-709)."""
+
+    enable: bool = True
+    num_bits: int | tuple[int, int] | str = 8
+    effective_bits: float | None = None
+    axis: int | tuple[int, ...] | None = None
+    fake_quant: bool = True
+    unsigned: bool = False
+    narrow_range: bool = False  # reference default False (config.py:459-463)
+    learn_amax: bool = False
+    type: str = Field(default="static", pattern=r"^static$|^dynamic$")
+    block_sizes: dict | None = None
+    bias: dict | None = None
+    trt_high_precision_dtype: str = Field(default="Float", pattern=r"^Float$|^Half$|^BFloat16$")
+    calibrator: Any = "max"
+    rotate: Any = False
+    pass_through_bwd: bool = True
+    backend: str | None = None
+    backend_extra_args: dict | None = None
+    use_constant_amax: bool = False
+    constant_amax: float | None = None
+
+    @model_validator(mode="before")
+    @classmethod
+    def _validate_config(cls, values):
+        if isinstance(values, Mapping):
+            values = dict(values)
+            if len(values) == 1 and values.get("enable") is True:
+                raise ValueError(
+                    "Invalid quantizer config: Cannot specify only {'enable': True}. "
+                    "Additional parameters are required when enabling quantization."
+                )
+            if "num_bits" in values:
+                values["num_bits"] = _parse_num_bits(values["num_bits"])
+            if "block_sizes" in values:
+                values["block_sizes"] = _parse_block_sizes(values["block_sizes"])
+            if isinstance(values.get("axis"), list):
+                values["axis"] = tuple(values["axis"])
+        return values
+
+    @field_validator("effective_bits")
+    @classmethod
+    def _validate_effective_bits(cls, v):
+        if v is not None and not (0 < v <= 16):
+            raise ValueError(f"effective_bits must be in (0, 16], got {v}")
+        return v
+
+    @field_validator("learn_amax")
+    @classmethod
+    def _validate_learn_amax(cls, v):
+        assert v is not True, "learn_amax is deprecated and reserved for backward compatibility."
+        return v
+
+    @field_validator("block_sizes")
+    @classmethod
+    def _validate_block_sizes(cls, v, info: ValidationInfo):
+        if v is None:
+            return v
+        assert info.data.get("axis") is None, "axis must be None when block_sizes is not None."
+        if v.get("type", None) == "dynamic":
+            assert len(cls._get_block_quant_axes_and_sizes(v)) == 1, (
+                "Dynamic block quantization only supports quantization last axis."
+            )
+        for k, val in v.items():
+            if isinstance(k, str):
+                assert k in ["type", "scale_bits", "scale_block_sizes", "four_over_six"]
+            else:
+                assert isinstance(k, int) and (val is None or isinstance(val, int))
+        return v
+
+    @field_validator("bias")
+    @classmethod
+    def _validate_bias(cls, v):
+        if v is None:
+            return v
+        if "type" in v and v["type"] not in ["static", "dynamic"]:
+            raise ValueError(f"Invalid bias type: {v['type']}, expected 'static' or 'dynamic'")
+        if "method" in v and v["method"] not in ["mean", "max_min"]:
+            raise ValueError(f"Invalid bias method: {v['method']}, expected 'mean' or 'max_min'")
+        axis = [k for k in v if k not in ["type", "method"]]
+        assert len(axis) > 0, "The axis for bias computation is not specified."
+        for x in axis:
+            if not isinstance(x, int):
+                raise ValueError(f"Invalid axis type {type(axis)}, expected int")
+        return v
+
+    @field_validator("calibrator")
+    @classmethod
+    def _validate_calibrator(cls, v):
+        if isinstance(v, str):
+            assert v in ["max", "histogram"]
+        return v
+
+    @field_validator("constant_amax")
+    @classmethod
+    def _validate_constant_amax(cls, v):
+        assert v is None or v > 0, "constant_amax must be a positive value."
+        return v
+
+    @model_validator(mode="after")
+    def _validate_num_bits(self):
+        if self.backend is not None:
+            return self
+        nb = self.num_bits
+        if isinstance(nb, int) and nb < 1:
+            raise ValueError(f"num_bits must be a positive integer or a tuple of positive integers. {nb}")
+        if isinstance(nb, tuple):
+            if not all(x >= 0 for x in nb) or not any(x > 0 for x in nb):
+                raise ValueError("num_bits must be a positive integer or a tuple of positive integers.")
+            if nb not in _FP_FORMATS:
+                raise ValueError(
+                    "Supported FPx quantization formats: FP8 (E4M3, E5M2), FP6(E3M2, E2M3), FP4(E2M1)."
+                )
+            bs = self.block_sizes
+            if nb not in [(4, 3), (2, 1)] and (bs is None or bs.get("type", None) != "dynamic"):
+                raise ValueError(
+                    "Only blockwise dynamic quantization is supported with quantization formats "
+                    f"E{nb[0]}M{nb[1]}."
+                )
+        assert not (self.use_constant_amax and self.constant_amax is not None), (
+            "use_constant_amax and constant_amax are mutually exclusive; set only one."
+        )
+        return self
+
+    @staticmethod
+    def _get_block_quant_axes_and_sizes(block_sizes):
+        if block_sizes is None:
+            return None
+        return {
+            k: v
+            for k, v in block_sizes.items()
+            if k not in ["type", "scale_bits", "scale_block_sizes", "four_over_six"]
+        }
+
+
+class QuantizerCfgEntry(_Config):
+    """One entry of an ordered ``quant_cfg`` list (reference config.py:165-243)."""
+
+    quantizer_name: str
+    parent_class: str | None = None
+    cfg: QuantizerAttributeConfig | list[QuantizerAttributeConfig] | None = None
+    enable: bool = True
+
+    @model_validator(mode="before")
+    @classmethod
+    def _normalize_cfg_shape(cls, values):
+        if not isinstance(values, dict):
+            return values
+        cfg = values.get("cfg")
+        empty = (isinstance(cfg, dict) and len(cfg) == 0) or (
+            isinstance(cfg, list)
+            and (len(cfg) == 0 or all(isinstance(i, dict) and len(i) == 0 for i in cfg))
+        )
+        if empty:
+            if values.get("enable") is False:
+                values = {**values, "cfg": None}
+            else:
+                raise ValueError(
+                    f"QuantizerCfgEntry 'cfg' must specify at least one quantizer attribute; got an "
+                    f"empty mapping/list for quantizer {values.get('quantizer_name')!r}."
+                )
+        return values
+
+    @model_validator(mode="after")
+    def _validate_instruction(self):
+        if "cfg" not in self.model_fields_set and "enable" not in self.model_fields_set:
+            raise ValueError(
+                "QuantizerCfgEntry must specify 'cfg', 'enable', or both "
+                f"(quantizer_name={self.quantizer_name!r})."
+            )
+        return self
+
+
+def normalize_quant_cfg_list(quant_cfg) -> list[dict[str, Any]]:
+    """Normalise a quant_cfg (ordered list of entries, or a legacy {pattern: cfg} dict) to a list of
+    ``{"quantizer_name", "parent_class", "cfg", "enable"}`` dicts with explicit ``enable``/``cfg``
+    (reference config.py:1447-1571)."""
+    if quant_cfg is None:
+        return []
+    entries: list = []
+    if isinstance(quant_cfg, Mapping):
+        # legacy dict form: {"*weight_quantizer": {...}, "default": {...}, "nn.Linear": {"*": ...}}
+        for k, v in quant_cfg.items():
+            if k == "default":
+                k = "*"
+            if isinstance(v, Mapping) and k.startswith("nn.") and all(isinstance(kk, str) for kk in v):
+                for kk, vv in v.items():
+                    entries.append(_legacy_entry(kk, vv, parent_class=k))
+                continue
+            entries.append(_legacy_entry(k, v))
+    else:
+        entries = list(quant_cfg)
+    out = []
+    for e in entries:
+        if isinstance(e, QuantizerCfgEntry):
+            e = {k: getattr(e, k) for k in e.model_fields_set | {"quantizer_name"}}
+        e = dict(e)
+        QuantizerCfgEntry(**e)  # validate shape
+        cfg = e.get("cfg")
+        if isinstance(cfg, Mapping) and len(cfg) == 0 and e.get("enable") is False:
+            cfg = None
+        enable = e.get("enable", True)
+        if isinstance(cfg, QuantizerAttributeConfig):
+            cfg = {k: getattr(cfg, k) for k in cfg.model_fields_set}
+        elif isinstance(cfg, list):
+            cfg = [
+                {k: getattr(c, k) for k in c.model_fields_set} if isinstance(c, QuantizerAttributeConfig) else dict(c)
+                for c in cfg
+            ]
+        elif isinstance(cfg, Mapping):
+            cfg = dict(cfg)
+            if "enable" in cfg:  # legacy: enable inside cfg
+                enable = cfg.pop("enable") if "enable" not in e else enable
+                if not cfg:
+                    cfg = None
+        out.append(
+            {
+                "quantizer_name": e["quantizer_name"],
+                "parent_class": e.get("parent_class"),
+                "cfg": cfg,
+                "enable": enable,
+            }
+        )
+    return out
+
+
+def _legacy_entry(name, v, parent_class=None):
+    e: dict[str, Any] = {"quantizer_name": name}
+    if parent_class:
+        e["parent_class"] = parent_class
+    if isinstance(v, Mapping) and set(v.keys()) == {"enable"}:
+        e["enable"] = v["enable"]
+    else:
+        if isinstance(v, Mapping) and "enable" in v:
+            v = dict(v)
+            e["enable"] = v.pop("enable")
+        e["cfg"] = v
+    return e
+
+
+class QuantizeAlgorithmConfig(_Config):
+    """Base calibration-algorithm config (reference config.py:780)."""
+
+    model_config = ConfigDict(extra="allow", validate_assignment=True, arbitrary_types_allowed=True)
+    method: str | None = None
+    moe_calib_experts_ratio: float | None = None
+    layerwise: Any = None
+
+
+class MaxCalibConfig(QuantizeAlgorithmConfig):
+    method: str | None = "max"
+    distributed_sync: bool | None = True
+    sync_expert_weight_amax: bool = False
+    shared_states: Any = None
+
+
+class AWQLiteCalibConfig(QuantizeAlgorithmConfig):
+    method: str | None = "awq_lite"
+    alpha_step: float = Field(default=0.1, gt=0.0, le=1.0)
+    debug: bool = False
+
+
+class AWQClipCalibConfig(QuantizeAlgorithmConfig):
+    method: str | None = "awq_clip"
+    max_co_batch_size: int = 1024
+    max_tokens_per_batch: int = 64
+    min_clip_ratio: float = 0.5
+    shrink_step: float = 0.05
+    debug: bool = False
+
+
+class AWQFullCalibConfig(AWQLiteCalibConfig, AWQClipCalibConfig):
+    method: str | None = "awq_full"
+
+
+_ALGO_CONFIGS: dict[str, type[QuantizeAlgorithmConfig]] = {
+    "max": MaxCalibConfig,
+    "awq_lite": AWQLiteCalibConfig,
+    "awq_clip": AWQClipCalibConfig,
+    "awq_full": AWQFullCalibConfig,
+}
+
+
+def algorithm_config(algorithm) -> QuantizeAlgorithmConfig | None:
+    if algorithm is None:
+        return None
+    if isinstance(algorithm, QuantizeAlgorithmConfig):
+        return algorithm
+    if isinstance(algorithm, str):
+        algorithm = {"method": algorithm}
+    algorithm = dict(algorithm)
+    method = algorithm.get("method")
+    cls = _ALGO_CONFIGS.get(method)
+    if cls is None:
+        raise NotImplementedError(
+            f"modelopt_amd: calibration algorithm {method!r} is outside the MI355X-native hot path "
+            "(supported: max, awq_lite, awq_clip, awq_full)"
+        )
+    return cls(**algorithm)
+
+
+class QuantizeConfig(_Config):
+    """``{"quant_cfg": [...], "algorithm": ...}`` (reference config.py:1573)."""
+
+    quant_cfg: Any = Field(default_factory=list)
+    algorithm: Any = "max"
+
+    @field_validator("quant_cfg")
+    @classmethod
+    def _normalize(cls, v):
+        return normalize_quant_cfg_list(v)
+
+
+def need_calibration(config) -> bool:
+    """Whether a config needs a calibration forward (reference config.py:1827)."""
+    cfg = config if isinstance(config, Mapping) else config.model_dump()
+    algo = cfg.get("algorithm")
+    if algo is not None and (algo if isinstance(algo, str) else algo.get("method")) not in (None, "max"):
+        return True
+    for e in normalize_quant_cfg_list(cfg.get("quant_cfg", [])):
+        c = e["cfg"]
+        if not e["enable"] or c is None:
+            continue
+        cs = c if isinstance(c, list) else [c]
+        for ci in cs:
+            bs = ci.get("block_sizes") or {}
+            if ci.get("type", "static") == "static" and bs.get("type", "static") == "static":
+                if "input_quantizer" in e["quantizer_name"] or "output_quantizer" in e["quantizer_name"]:
+                    return True
+    return False
+
+
+def choices(config: Mapping) -> Mapping:
+    return config
+
+
+# ----------------------------------------------------------------------------------------------
+# Presets.  Entry lists equal to the reference's YAML-composed presets
+# (modelopt_recipes/configs/ptq/units/{base_disable_all,default_disabled_quantizers}.yaml + the
+# per-format numerics units); printed from the reference in SURVEY §8.
+# ----------------------------------------------------------------------------------------------
+
+_BASE_DISABLE_ALL = [{"quantizer_name": "*", "enable": False}]
+
+_DEFAULT_DISABLED_QUANTIZERS = [
+    {"quantizer_name": n, "enable": False}
+    for n in [
+        "*block_sparse_moe.gate*",
+        "*linear_attn.conv1d*",
+        "*linear_attn.in_proj_a*",
+        "*linear_attn.in_proj_b*",
+        "*lm_head*",
+        "*mixer.conv1d*",
+        "*mlp.gate.*",
+        "*mlp.shared_expert_gate.*",
+        "*output_layer*",
+        "*proj_out.*",
+        "*router*",
+        "mtp.*",
+        "output.*",
+        "*embed_vision*",
+        "*vision_tower*",
+        "*visual*",
+        "*vision_model*",
+        "*multi_modal_projector*",
+    ]
+] + [
+    {"quantizer_name": "*", "parent_class": c, "enable": False}
+    for c in ["nn.BatchNorm1d", "nn.BatchNorm2d", "nn.BatchNorm3d", "nn.LeakyReLU", "nn.Embedding"]
+]
+
+
+def _preset(weight, inp, algorithm="max") -> dict[str, Any]:
+    qc = list(_BASE_DISABLE_ALL)
+    if weight is not None:
+        qc.append({"quantizer_name": "*weight_quantizer", "cfg": weight})
+    if inp is None:
+        qc.append({"quantizer_name": "*input_quantizer", "enable": False})
+    elif inp != "keep":
+        qc.append({"quantizer_name": "*input_quantizer", "cfg": inp})
+    qc += _DEFAULT_DISABLED_QUANTIZERS
+    return {"quant_cfg": copy.deepcopy(qc), "algorithm": copy.deepcopy(algorithm)}
+
+
+_MX = lambda nb: {"num_bits": nb, "block_sizes": {-1: 32, "type": "dynamic", "scale_bits": (8, 0)}}  # noqa: E731
+
+INT8_DEFAULT_CFG: dict[str, Any] = _preset({"num_bits": 8, "axis": 0}, {"num_bits": 8, "axis": None})
+INT8_WEIGHT_ONLY_CFG: dict[str, Any] = _preset({"num_bits": 8, "axis": 0}, None)
+FP8_DEFAULT_CFG: dict[str, Any] = _preset(
+    {"num_bits": (4, 3), "axis": None}, {"num_bits": (4, 3), "axis": None}
+)
+FP8_PER_CHANNEL_PER_TOKEN_CFG: dict[str, Any] = _preset(
+    {"num_bits": (4, 3), "axis": 0},
+    {"num_bits": (4, 3), "axis": None, "type": "dynamic", "block_sizes": {-1: None}},
+)
+FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG: dict[str, Any] = _preset(
+    {"num_bits": (4, 3), "axis": None, "block_sizes": {-1: 128, -2: 128}}, None
+)
+INT4_BLOCKWISE_WEIGHT_ONLY_CFG: dict[str, Any] = _preset(
+    {"num_bits": 4, "block_sizes": {-1: 128, "type": "static"}}, None
+)
+INT4_AWQ_CFG: dict[str, Any] = _preset(
+    {"num_bits": 4, "block_sizes": {-1: 128, "type": "static"}},
+    None,
+    {"method": "awq_lite", "alpha_step": 0.1},
+)
+MXFP8_DEFAULT_CFG: dict[str, Any] = _preset(_MX((4, 3)), _MX((4, 3)), None)
+MXFP6_DEFAULT_CFG: dict[str, Any] = _preset(_MX((3, 2)), _MX((3, 2)), None)
+MXFP4_DEFAULT_CFG: dict[str, Any] = _preset(_MX((2, 1)), _MX((2, 1)), None)
+MXINT8_DEFAULT_CFG: dict[str, Any] = _preset(_MX(8), _MX(8), None)
+W4A8_MXFP4_FP8_CFG: dict[str, Any] = _preset(_MX((2, 1)), {"num_bits": (4, 3), "axis": None}, None)
+MXFP4_MLP_WEIGHT_ONLY_CFG: dict[str, Any] = {
+    "quant_cfg": _BASE_DISABLE_ALL
+    + [
+        {"quantizer_name": "*mlp*weight_quantizer", "cfg": _MX((2, 1))},
+        {"quantizer_name": "*block_sparse_moe*weight_quantizer", "cfg": _MX((2, 1))},
+    ]
+    + _DEFAULT_DISABLED_QUANTIZERS,
+    "algorithm": None,
+}
+
+__all__ += [
+    "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG",
+    "FP8_DEFAULT_CFG",
+    "FP8_PER_CHANNEL_PER_TOKEN_CFG",
+    "INT4_AWQ_CFG",
+    "INT4_BLOCKWISE_WEIGHT_ONLY_CFG",
+    "INT8_DEFAULT_CFG",
+    "INT8_WEIGHT_ONLY_CFG",
+    "MXFP4_DEFAULT_CFG",
+    "MXFP4_MLP_WEIGHT_ONLY_CFG",
+    "MXFP6_DEFAULT_CFG",
+    "MXFP8_DEFAULT_CFG",
+    "MXINT8_DEFAULT_CFG",
+    "W4A8_MXFP4_FP8_CFG",
+]
+
+ForwardLoop = Callable[[Any], Any]

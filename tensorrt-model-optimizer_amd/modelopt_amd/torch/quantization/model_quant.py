@@ -1,0 +1,138 @@
+"""User-facing PTQ API: ``mtq.quantize`` / ``mtq.calibrate`` (reference: model_quant.py).
+
+``quantize(model, config, forward_loop)`` = convert (insert quantizers, apply the ordered
+wildcard ``quant_cfg``) + ``calibrate(model, config["algorithm"], forward_loop)``, as in
+model_quant.py:147-250.  The reference routes both through its mode framework (apply_mode /
+QuantizeModeDescriptor, mode.py); here they are direct calls with the same effects, and the
+quantizer state is recorded on ``model._modelopt_amd_state`` for save/restore.
+"""
+
+from __future__ import annotations
+
+import fnmatch
+import inspect
+import warnings
+from collections.abc import Callable
+from typing import Any
+
+import torch
+import torch.nn as nn
+
+from .config import QuantizeConfig, algorithm_config
+from .conversion import convert_to_quantized_model, quantizer_state, set_quantizer_attributes_partial
+from .model_calib import awq, max_calibrate
+from .nn.modules.quant_module import QuantModule
+from .nn.modules.tensor_quantizer import SequentialQuantizer, TensorQuantizer
+from .utils.names import is_quantized
+
+__all__ = [
+    "calibrate",
+    "disable_quantizer",
+    "enable_quantizer",
+    "fold_weight",
+    "postprocess_amax",
+    "print_quant_summary",
+    "quantize",
+]
+
+
+def _apply_algorithm(model, algo_cfg, forward_loop):
+    if algo_cfg is None:
+        return
+    kwargs = algo_cfg.model_dump()
+    method = kwargs.pop("method")
+    kwargs.pop("moe_calib_experts_ratio", None)
+    layerwise = kwargs.pop("layerwise", None)
+    if layerwise and (layerwise is True or (isinstance(layerwise, dict) and layerwise.get("enable"))):
+        raise NotImplementedError("modelopt_amd: layerwise calibration is a next-round item")
+    if method == "max":
+        kwargs.pop("shared_states", None)
+        max_calibrate(model, forward_loop, **kwargs)
+    elif method in ("awq_lite", "awq_full", "awq_clip"):
+        awq(model, forward_loop, algorithm=method, **kwargs)
+    elif method is None:
+        return
+    else:
+        raise NotImplementedError(f"calibration algorithm {method!r}")
+
+
+def calibrate(model: nn.Module, algorithm="max", forward_loop: Callable | None = None) -> nn.Module:
+    """Calibrate the quantizers of ``model`` (reference :64-129)."""
+    if forward_loop is not None:
+        nargs = len(inspect.signature(forward_loop).parameters)
+        if nargs == 0:
+            warnings.warn(
+                "forward_loop should take model as argument, but got forward_loop without any arguments.",
+                DeprecationWarning,
+            )
+            original = forward_loop
+
+            def forward_loop(model):  # noqa: F811
+                return original()
+
+    is_training = model.training
+    model.eval()
+    _apply_algorithm(model, algorithm_config(algorithm), forward_loop)
+    for name, module in model.named_modules():
+        if isinstance(module, TensorQuantizer):
+            for attr_name in ["_amax", "_pre_quant_scale"]:
+                module.validate_attr(attr_name=attr_name, warn_error=True, name=name)
+    model.train(is_training)
+    model.__dict__["_modelopt_amd_state"] = {"quantizer_state": quantizer_state(model)}
+    return model
+
+
+def quantize(model: nn.Module, config: dict[str, Any] | QuantizeConfig, forward_loop: Callable | None = None) -> nn.Module:
+    """Quantize and calibrate ``model`` in place (reference :147-250)."""
+    if isinstance(config, dict):
+        config = QuantizeConfig(**config)
+    if not is_quantized(model):
+        convert_to_quantized_model(model, config)
+    else:
+        from .conversion import set_quantizer_by_cfg
+
+        set_quantizer_by_cfg(model, config.quant_cfg)
+    return calibrate(model, config.algorithm, forward_loop)
+
+
+def postprocess_amax(model: nn.Module, key: str, post_process_fn) -> nn.Module:
+    """Apply ``post_process_fn`` to the amax of quantizers matching ``key`` (reference :132-145)."""
+    for name, module in model.named_modules():
+        if not isinstance(module, TensorQuantizer) or not fnmatch.fnmatch(name, key):
+            continue
+        if module.amax is not None:
+            module.amax = post_process_fn(module.amax)
+    return model
+
+
+def disable_quantizer(model: nn.Module, wildcard_or_filter_func: str | Callable):
+    set_quantizer_attributes_partial(model, wildcard_or_filter_func, {"enable": False})
+
+
+def enable_quantizer(model: nn.Module, wildcard_or_filter_func: str | Callable):
+    set_quantizer_attributes_partial(model, wildcard_or_filter_func, {"enable": True})
+
+
+def print_quant_summary(model: nn.Module, output_dir: str | None = None):
+    lines = []
+    for name, mod in model.named_modules():
+        if isinstance(mod, (TensorQuantizer, SequentialQuantizer)):
+            lines.append(f"{name:80} {mod}")
+    lines.append(f"{len(lines)} TensorQuantizers found in model")
+    text = "\n".join(lines)
+    if output_dir:
+        import os
+
+        os.makedirs(output_dir, exist_ok=True)
+        with open(os.path.join(output_dir, ".quant_summary.txt"), "w") as f:
+            f.write(text)
+    else:
+        print(text)
+
+
+@torch.no_grad()
+def fold_weight(model: nn.Module, keep_attrs: bool = False):
+    """Bake the weight fake-quant into the weights (reference :728-738)."""
+    for _, module in model.named_modules():
+        if isinstance(module, QuantModule):
+            module.fold_weight(keep_attrs)

@@ -1,0 +1,846 @@
+"""TensorQuantizer: the calibrate / fake-quantise state machine over the HIP kernels.
+
+Mirrors modelopt/torch/quantization/nn/modules/tensor_quantizer.py (TensorQuantizer :136-1420,
+StaticBlockScaleQuantizer :1484-1731, SequentialQuantizer :1834-1892, the backend registry
+:92-129): same attribute names, properties, buffers (``_amax``, ``_pre_quant_scale``), state dict
+and ``get_modelopt_state`` layout, same forward order (pre-quant scale, disable check,
+block-sizes-to-axis, static-block reshape, collect, fake quant, reshape back).
+
+MI355X-specific behaviour:
+* fake quant dispatches straight to the ``modelopt_amd`` ops; under ``no_grad`` / for inputs that
+  do not require grad the autograd Function is bypassed (its STE backward is not needed), which
+  removes ~10 us of Python per call on the 448 quantizer calls per Llama-3-8B forward;
+* calibration uses the fused accumulate-max kernel (calib/max.py) -- one launch per collect;
+* out of scope for the hot path (raise ``NotImplementedError``): real quantisation / compress,
+  rotation (Hadamard), affine bias calibration, NVFP4 two-level static block scales, LSQ.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import math
+import warnings
+from collections.abc import Callable
+from typing import Any
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ... import calib
+from ...config import QuantizerAttributeConfig
+from ...tensor_quant import (
+    DynamicBlockQuantizationFunction,
+    FakeTensorQuantFunction,
+    ScaledE4M3Function,
+    _dynamic_block_quantize_forward,
+    fp8_fake_quant,
+    quantize_op,
+)
+from ...utils import core_utils as quant_utils
+
+__all__ = [
+    "SequentialQuantizer",
+    "StaticBlockScaleQuantizer",
+    "TensorQuantizer",
+    "is_registered_quant_backend",
+    "register_quant_backend",
+    "unregister_quant_backend",
+]
+
+QuantBackendEntrypoint = Callable[[torch.Tensor, "TensorQuantizer"], torch.Tensor]
+_QUANT_FUNCTIONAL_BACKENDS: dict[str, QuantBackendEntrypoint] = {}
+
+
+def register_quant_backend(name: str, entrypoint: QuantBackendEntrypoint) -> None:
+    """Register a custom quantization backend (reference :92-109)."""
+    if not isinstance(name, str) or not name:
+        raise ValueError("Backend name must be a non-empty string.")
+    if not callable(entrypoint):
+        raise TypeError("Entrypoint must be callable.")
+    if name in _QUANT_FUNCTIONAL_BACKENDS:
+        warnings.warn(f"Overwriting existing backend: {name}")
+    _QUANT_FUNCTIONAL_BACKENDS[name] = entrypoint
+
+
+def unregister_quant_backend(name: str) -> None:
+    if not isinstance(name, str) or not name:
+        raise ValueError("Backend name must be a non-empty string.")
+    _QUANT_FUNCTIONAL_BACKENDS.pop(name, None)
+
+
+def is_registered_quant_backend(name: str) -> bool:
+    return name in _QUANT_FUNCTIONAL_BACKENDS
+
+
+def _standardize_constructor_args(val):
+    """(cls, args, kwargs) from a calibrator 'constructor-like' (modelopt.torch.utils)."""
+    if isinstance(val, type):
+        return val, (), {}
+    if isinstance(val, (tuple, list)):
+        cls = val[0]
+        args = tuple(val[1]) if len(val) > 1 and val[1] is not None else ()
+        kwargs = dict(val[2]) if len(val) > 2 and val[2] is not None else {}
+        return cls, args, kwargs
+    if isinstance(val, dict):
+        return val["cls"], tuple(val.get("args", ())), dict(val.get("kwargs", {}))
+    raise TypeError(f"Unsupported calibrator constructor {val!r}")
+
+
+class TensorQuantizer(nn.Module):
+    """Tensor quantizer module (reference :136)."""
+
+    _skip_properties_for_save_restore = {
+        "_calibrator",
+        "_bias_calibrator",
+        "_original_shape",
+        "_block_reshape_size",
+        "_padding",
+        "_is_hf_initialized",
+        "_hf_hook",
+        "_old_forward",
+        "forward",
+        "_quantizer_cache",
+        "_shared_quant_tied_attrs",
+    }
+
+    def __init__(self, quant_attribute_cfg=None, if_quant=True, if_calib=False, amax=None):
+        super().__init__()
+        quant_attribute_cfg = (
+            quant_attribute_cfg if quant_attribute_cfg is not None else QuantizerAttributeConfig()
+        )
+        if amax is not None:
+            self.amax = amax
+        self._use_constant_amax = False
+        self._constant_amax = None
+        self.set_from_attribute_config(quant_attribute_cfg)
+        self._if_quant = if_quant
+        self._if_calib = if_calib
+        self._enable_pre_quant_scale = True
+        self._dequantize = False
+        self._input_dtype = None
+        self._bias_calibrator = None
+        self._quantizer_cache = None
+
+    # ---- configuration --------------------------------------------------------------------
+    def set_from_attribute_config(self, attribute_cfg: QuantizerAttributeConfig | dict[str, Any]):
+        """Set quantizer attributes from attribute_cfg (reference :228-290)."""
+        if isinstance(attribute_cfg, dict):
+            # validate like the reference (pydantic) but apply only the keys that were given
+            QuantizerAttributeConfig(**attribute_cfg)
+            items = QuantizerAttributeConfig.model_validate(attribute_cfg).model_dump(
+                include=set(attribute_cfg.keys())
+            ).items()
+        else:
+            items = attribute_cfg.items()
+
+        def _calibrator_setter(val):
+            if val in ["max", "histogram"]:
+                cls = calib.MaxCalibrator if val == "max" else calib.HistogramCalibrator
+                args, kwargs = (self._num_bits, self._axis, self._unsigned), {}
+            else:
+                cls, args, kwargs = _standardize_constructor_args(val)
+            return cls(*args, **kwargs)
+
+        def _axis_setter(val):
+            if getattr(self, "_calibrator", None) is not None:
+                self._calibrator._axis = val
+            return val
+
+        def _block_sizes_setter(val):
+            if val is not None:
+                self._axis = None
+                if getattr(self, "_calibrator", None) is not None:
+                    self._calibrator._axis = None
+            return val
+
+        def _constant_amax_setter(val):
+            if val is not None:
+                self.amax = float(val)
+            return val
+
+        custom: dict[str, tuple[str, Callable]] = {
+            "enable": ("_disabled", lambda v: v is False),
+            "type": ("_dynamic", lambda v: v == "dynamic"),
+            "calibrator": ("_calibrator", _calibrator_setter),
+            "axis": ("_axis", _axis_setter),
+            "block_sizes": ("_block_sizes", _block_sizes_setter),
+            "backend": ("backend", lambda v: v),
+            "backend_extra_args": ("backend_extra_args", lambda v: v or {}),
+            "use_constant_amax": ("_use_constant_amax", lambda v: v),
+            "constant_amax": ("_constant_amax", _constant_amax_setter),
+        }
+        items = list(items)
+        # num_bits / axis / unsigned must be set before the calibrator is constructed
+        order = {"num_bits": 0, "axis": 1, "unsigned": 2, "block_sizes": 3, "calibrator": 9}
+        items.sort(key=lambda kv: order.get(kv[0], 5))
+        for attribute, val in items:
+            assert attribute in QuantizerAttributeConfig.model_fields, (
+                f"{attribute} is not a valid `TensorQuantizer` attribute"
+            )
+            name, setter = custom.get(attribute, (f"_{attribute}", lambda v: v))
+            setattr(self, name, setter(val))
+        if self._rotate_enabled():
+            raise NotImplementedError("modelopt_amd: input rotation (QuaRot/SpinQuant) is out of scope")
+        if getattr(self, "_bias", None):
+            raise NotImplementedError("modelopt_amd: affine bias calibration is out of scope")
+        if self.is_mx_format:
+            self._pass_through_bwd = True
+
+    def _rotate_enabled(self):
+        r = getattr(self, "_rotate", False)
+        if isinstance(r, dict):
+            return bool(r.get("enable", False))
+        if hasattr(r, "enable"):
+            return bool(r.enable)
+        return bool(r)
+
+    # ---- properties -------------------------------------------------------------------------
+    @property
+    def num_bits(self):
+        return self._num_bits
+
+    @num_bits.setter
+    def num_bits(self, value):
+        self._num_bits = value
+        self._calibrator._num_bits = value
+
+    @property
+    def maxbound(self):
+        if self._num_bits == (4, 3):
+            return 448.0
+        if self._num_bits == (2, 1) and (self._block_sizes or {}).get("scale_bits") == (4, 3):
+            return 6.0
+        return (1 << (self._num_bits - 1 + int(self._unsigned))) - 1
+
+    @property
+    def unsigned(self):
+        return self._unsigned
+
+    @unsigned.setter
+    def unsigned(self, value):
+        self._unsigned = value
+        self._calibrator._unsigned = value
+
+    @property
+    def pre_quant_scale(self):
+        if not hasattr(self, "_pre_quant_scale") or not self._enable_pre_quant_scale:
+            return None
+        return self._pre_quant_scale
+
+    @pre_quant_scale.setter
+    def pre_quant_scale(self, value):
+        assert value is not None, "pre_quant_scale cannot be set to None."
+        assert self._enable_pre_quant_scale, (
+            "pre_quant_scale cannot be set when forward_with_pre_quant_scale is False."
+        )
+        if not isinstance(value, torch.Tensor):
+            value = torch.tensor(value)
+        if not hasattr(self, "_pre_quant_scale"):
+            self.register_buffer("_pre_quant_scale", value.clone().detach())
+        else:
+            if self._pre_quant_scale.shape != value.shape:
+                raise RuntimeError("Changing shape when setting pre_quant_scale is not allowed.")
+            self._pre_quant_scale.data.copy_(value.clone().detach().to(self._pre_quant_scale.device))
+
+    @property
+    def amax(self):
+        if not hasattr(self, "_amax") or self.is_mx_format:
+            return None
+        assert not self._dynamic, "Dynamic quantization does not have fixed amax"
+        return self._amax
+
+    @amax.setter
+    def amax(self, value):
+        assert value is not None, "amax cannot be set to None."
+        if not isinstance(value, torch.Tensor):
+            value = torch.tensor(value)
+        self._amax_setter_helper(value)
+
+    def _amax_setter_helper(self, value):
+        if not hasattr(self, "_amax"):
+            self.register_buffer("_amax", value.clone().detach())
+        else:
+            if self._amax.shape != value.shape:
+                raise RuntimeError("Changing shape when setting amax is not allowed.")
+            self._amax.data.copy_(value.clone().detach().to(self._amax.device))
+
+    def reset_amax(self):
+        if hasattr(self, "_amax"):
+            delattr(self, "_amax")
+        self._calibrator.reset()
+
+    def reset_bias(self):
+        if hasattr(self, "_bias_value"):
+            delattr(self, "_bias_value")
+
+    @property
+    def step_size(self):
+        if not hasattr(self, "_amax"):
+            warnings.warn("step_size is undefined under dynamic amax mode!")
+            return None
+        assert isinstance(self._num_bits, int), "Step size is not defined for non-integer quantization."
+        return self._amax / (2.0 ** (self._num_bits - 1 + int(self._unsigned)) - 1.0)
+
+    @property
+    def axis(self):
+        return self._axis
+
+    @axis.setter
+    def axis(self, value):
+        self._axis = value
+        self._calibrator._axis = value
+
+    @property
+    def block_sizes(self):
+        return self._block_sizes
+
+    @block_sizes.setter
+    def block_sizes(self, value):
+        self._axis = None
+        self._block_sizes = value
+
+    @property
+    def bias(self):
+        return getattr(self, "_bias", None)
+
+    @property
+    def bias_calibrator(self):
+        return None
+
+    @property
+    def fake_quant(self):
+        return self._fake_quant
+
+    @property
+    def narrow_range(self):
+        return self._narrow_range
+
+    @narrow_range.setter
+    def narrow_range(self, value):
+        self._narrow_range = value
+
+    @property
+    def is_enabled(self):
+        return not self._disabled
+
+    def disable(self):
+        self._disabled = True
+
+    def enable(self):
+        self._disabled = False
+
+    @property
+    def trt_high_precision_dtype(self):
+        return self._trt_high_precision_dtype
+
+    @trt_high_precision_dtype.setter
+    def trt_high_precision_dtype(self, value):
+        self._trt_high_precision_dtype = value
+
+    @property
+    def is_mx_format(self):
+        return (
+            self.block_sizes is not None
+            and self.block_sizes.get("type", None) == "dynamic"
+            and self.block_sizes.get("scale_bits", None) == (8, 0)
+        )
+
+    @property
+    def is_fp8(self):
+        return self._num_bits == (4, 3) and self._block_sizes is None and self._axis is None
+
+    @property
+    def is_nvfp4_dynamic(self):
+        return (
+            self._block_sizes is not None
+            and self._block_sizes.get("type", None) == "dynamic"
+            and self._num_bits == (2, 1)
+            and self._block_sizes.get("scale_bits", None) == (4, 3)
+        )
+
+    @property
+    def is_nvfp4_static(self):
+        return (
+            self.is_static_block_quant
+            and self._num_bits == (2, 1)
+            and self._block_sizes is not None
+            and self._block_sizes.get("scale_bits") == (4, 3)
+        )
+
+    def is_mxfp(self, bits):
+        fmt = {4: (2, 1), 6: (3, 2), 8: (4, 3)}
+        if bits not in fmt:
+            raise NotImplementedError()
+        return self.is_mx_format and self.num_bits == fmt[bits] and self.block_sizes.get(-1, None) == 32
+
+    @property
+    def is_static_block_quant(self):
+        return (
+            self.block_sizes is not None
+            and self.block_sizes.get("type", None) != "dynamic"
+            and self._fake_quant
+        )
+
+    @property
+    def rotate_is_enabled(self):
+        return self._rotate_enabled()
+
+    def disable_rotate(self):
+        self._rotate = False
+
+    def disable_calib(self):
+        self._if_calib = False
+
+    def enable_calib(self):
+        if self._calibrator is None:
+            raise ValueError("Calibrator was not created, cannot enable calibration.")
+        if self._dynamic:
+            return
+        self._if_calib = True
+
+    def disable_quant(self):
+        self._if_quant = False
+
+    def enable_quant(self):
+        self._if_quant = True
+
+    def load_calib_amax(self, *args, **kwargs):
+        """Load amax from the calibrator (reference :693-720)."""
+        assert not self._dynamic, "Dynamic quantization does not need calibration."
+        strict = kwargs.pop("strict", True)
+        if getattr(self, "_calibrator", None) is None:
+            raise RuntimeError("Calibrator not created.")
+        calib_amax = self._calibrator.compute_amax(*args, **kwargs)
+        if calib_amax is None:
+            err = (
+                "Calibrator returned None. This usually happens when calibrator hasn't seen any tensor."
+            )
+            if not strict:
+                warnings.warn(err)
+                warnings.warn("Set amax to NaN!")
+                calib_amax = torch.tensor(math.nan)
+            else:
+                raise RuntimeError(
+                    err + " Passing 'strict=False' to `load_calib_amax()` will ignore the error."
+                )
+        self.amax = calib_amax
+
+    def _get_amax(self, inputs):
+        if self._use_constant_amax:
+            return torch.tensor(torch.finfo(torch.float8_e4m3fn).max, device=inputs.device)
+        if hasattr(self, "_amax"):
+            amax = self._amax
+            if amax.device != inputs.device:
+                amax = amax.to(inputs.device)
+        else:
+            reduce_axis = quant_utils.convert_quantization_axis_to_reduce_axis(inputs, self._axis)
+            amax = quant_utils.reduce_amax(inputs, axis=reduce_axis, keepdims=True).detach()
+        return amax.data
+
+    def validate_attr(self, attr_value=None, attr_name="amax", raise_error=False, warn_error=False, name=""):
+        attr_value = attr_value if attr_value is not None else getattr(self, attr_name, None)
+        if attr_value is None or (isinstance(attr_value, torch.Tensor) and attr_value.is_meta):
+            return True
+        is_valid = (
+            torch.all(attr_value >= 0)
+            and not torch.any(torch.isinf(attr_value))
+            and not torch.any(torch.isnan(attr_value))
+        )
+        if is_valid:
+            return True
+        name = f"{name}." if name else ""
+        msg = f"{name}{attr_name} contains invalid values: {attr_value}"
+        if warn_error:
+            warnings.warn(msg)
+        if raise_error:
+            raise ValueError(msg)
+        return False
+
+    # ---- fake quant ---------------------------------------------------------------------------
+    def _fake_quantize(self, inputs):
+        """Fake quantization (reference :890-949) on the HIP kernels."""
+        if self.backend is not None:
+            if self.backend not in _QUANT_FUNCTIONAL_BACKENDS:
+                raise KeyError(f"Quant backend '{self.backend}' is not registered.")
+            return _QUANT_FUNCTIONAL_BACKENDS[self.backend](inputs, self)
+
+        amax = None
+        if not self.is_mx_format:
+            amax = self._get_amax(inputs)
+        need_grad = torch.is_grad_enabled() and inputs.requires_grad
+
+        if self.block_sizes is not None and self.block_sizes.get("type", "static") == "dynamic":
+            block_size = self.block_sizes.get(-1, None) or self.block_sizes.get(inputs.dim() - 1, None)
+            if block_size is None:
+                raise ValueError("block size for dynamic quantization not found.")
+            if need_grad:
+                return DynamicBlockQuantizationFunction.apply(
+                    inputs, block_size, amax, None, self._num_bits,
+                    self.block_sizes.get("scale_bits", None), None, None, self._pass_through_bwd,
+                )
+            return _dynamic_block_quantize_forward(
+                None, inputs, block_size, amax, self._num_bits, self.block_sizes.get("scale_bits", None)
+            )
+        if isinstance(self._num_bits, tuple):
+            E, M = self._num_bits  # noqa: N806
+            if need_grad:
+                return ScaledE4M3Function.apply(inputs, amax, None, E, M, None, self._pass_through_bwd)
+            if E != 4 or M != 3:
+                raise NotImplementedError("Only support E=4 & M=3 for now.")
+            return fp8_fake_quant(inputs, amax)
+        if need_grad:
+            return FakeTensorQuantFunction.apply(
+                inputs, amax, None, self._num_bits, self._unsigned, self._narrow_range, None,
+                self._pass_through_bwd,
+            )
+        return quantize_op(inputs, amax, self._num_bits, 0, self._unsigned, self._narrow_range)
+
+    def _real_quantize(self, inputs):
+        raise NotImplementedError(
+            "modelopt_amd: real quantization (compress / qtensor) is outside the fake-quant hot path"
+        )
+
+    # ---- static block quant reshapes (reference :975-1085) ------------------------------------
+    def _setup_for_blockquant(self, inputs: torch.Tensor):
+        def get_axis_quant_params(ax):
+            ax = ax if ax in self.block_sizes else ax - inputs.dim()
+            bsize = self.block_sizes.get(ax, None)
+            padding, ax_slice = None, None
+            if bsize is not None and inputs.shape[ax] % bsize != 0:
+                padding = (bsize - (inputs.shape[ax] % bsize), 0)
+                ax_slice = slice(inputs.shape[ax])
+            return bsize, padding, ax_slice
+
+        def set_quant_params(axis, block_reshape_size, padding, slices, amax_shape=None):
+            self._axis = tuple(axis)
+            if hasattr(self, "_calibrator"):
+                self._calibrator._axis = self._axis
+            self._original_shape = inputs.shape
+            self._block_reshape_size = torch.Size(block_reshape_size)
+            if padding is not None:
+                self._padding = tuple(padding)
+                self._original_shape = F.pad(inputs, self._padding, "constant", 0).shape
+            if slices is not None:
+                self._slices = slices
+            if amax_shape:
+                self._amax_shape_for_export = amax_shape
+
+        if hasattr(self, "_block_reshape_size"):
+            return
+
+        reshape_size, quantize_axis, paddings, slices = [], [], [], []
+        if (self.block_sizes.get(inputs.dim() - 1, None) or self.block_sizes.get(-1, None)) and len(
+            QuantizerAttributeConfig._get_block_quant_axes_and_sizes(self.block_sizes)
+        ) == 1:
+            bsize, padding, ax_slice = get_axis_quant_params(inputs.dim() - 1)
+            slices = None if ax_slice is None else (*(slice(None),) * (inputs.dim() - 1), ax_slice)
+            padding = padding if not padding else tuple(reversed(padding))
+            amax_shape_for_export = (*(inputs.shape[:-1]), -1)
+            set_quant_params((0,), (-1, bsize), padding, slices, amax_shape_for_export)
+            return
+
+        for ax in range(inputs.dim()):
+            bsize, padding, ax_slice = get_axis_quant_params(ax)
+            paddings.append(padding)
+            slices.append(ax_slice)
+            if bsize is not None:
+                reshape_size.extend([math.ceil(inputs.shape[ax] / bsize), bsize])
+                quantize_axis.extend([True, False])
+            else:
+                reshape_size.append(inputs.shape[ax])
+                quantize_axis.append(True)
+        quant_axis = [i for i in range(len(quantize_axis)) if quantize_axis[i]]
+        slices = None if all(s is None for s in slices) else [s or slice(None) for s in slices]
+        if all(p is None for p in paddings):
+            paddings = None
+        else:
+            new_paddings = []
+            for padding in paddings:
+                if not (new_paddings or padding):
+                    continue
+                new_paddings.extend(padding or (0, 0))
+            paddings = tuple(reversed(new_paddings))
+        set_quant_params(quant_axis, reshape_size, paddings, slices)
+
+    def _process_for_blockquant(self, inputs: torch.Tensor):
+        if hasattr(self, "_padding"):
+            inputs = F.pad(inputs, self._padding, "constant", 0)
+        if inputs.shape != self._original_shape:
+            raise ValueError(
+                f"Input shape has changed from {self._original_shape} to {inputs.shape}."
+                " Block-quantization requires a fixed input shape."
+            )
+        return inputs.reshape(self._block_reshape_size)
+
+    def _reset_to_original_shape(self, outputs: torch.Tensor):
+        outputs = outputs.reshape(self._original_shape)
+        if hasattr(self, "_slices"):
+            outputs = outputs[self._slices]
+        return outputs
+
+    def _block_sizes_to_axis(self, x: torch.Tensor):
+        block_sizes = self._block_sizes
+        if block_sizes is None:
+            return
+        if all(v is None for k, v in block_sizes.items() if isinstance(k, int)):
+            assert self.axis is None, "Axis and block_sizes are both set."
+            axis = tuple(k if k >= 0 else k + x.dim() for k in block_sizes if isinstance(k, int))
+            self.axis = tuple(i for i in range(x.dim()) if i not in axis) or None
+            self._block_sizes = None
+
+    def export_amax(self) -> torch.Tensor | None:
+        if self.block_sizes is not None and self.block_sizes.get("type", None) == "dynamic":
+            return self.amax
+        if self.amax is None:
+            return None
+        amax = self.amax if not hasattr(self, "_amax_shape_for_export") else self.amax.reshape(
+            self._amax_shape_for_export
+        )
+        amax = amax.clone()
+        amax[amax == 0] = self.maxbound
+        amax = torch.nan_to_num(amax, nan=self.maxbound)
+        amax = amax.clamp(min=torch.finfo(amax.dtype).tiny, max=torch.finfo(amax.dtype).max)
+        if self.block_sizes is None:
+            if self.axis is None:
+                amax = amax.unsqueeze(0)
+            elif isinstance(self.axis, int) or (isinstance(self.axis, (list, tuple)) and len(self.axis) == 1):
+                amax = amax.squeeze()
+        return amax
+
+    # ---- forward --------------------------------------------------------------------------------
+    def forward(self, inputs):
+        """Quantize/calibrate ``inputs`` (reference :1119-1221)."""
+        if inputs.numel() == 0:
+            return inputs
+        if self.pre_quant_scale is not None:
+            inputs = inputs * self.pre_quant_scale
+        if self._disabled:
+            self._input_dtype = inputs.dtype if hasattr(inputs, "dtype") else None
+            return inputs
+        if self.block_sizes is not None and self._fake_quant:
+            self._block_sizes_to_axis(inputs)
+        static_block = self.is_static_block_quant
+        if static_block:
+            self._setup_for_blockquant(inputs)
+            inputs = self._process_for_blockquant(inputs)
+        outputs = inputs
+        if self._if_calib and not self._dynamic:
+            if self._calibrator is None:
+                raise RuntimeError("Calibrator was not created.")
+            self.collect(inputs)
+        if self._if_quant:
+            if not inputs.is_contiguous():
+                inputs = inputs.contiguous()
+            if self.fake_quant:
+                outputs = self._fake_quantize(inputs)
+            elif not self._dequantize:
+                outputs = self._real_quantize(inputs)
+            else:
+                raise ValueError("self._dequantize is True and self.fake_quant is False.")
+        if static_block:
+            outputs = self._reset_to_original_shape(outputs)
+        return outputs
+
+    def collect(self, inputs) -> None:
+        if not self._if_calib or self._dynamic:
+            return
+        self._calibrator.collect(inputs)
+
+    # ---- repr / state ---------------------------------------------------------------------------
+    def _short_amax(self, fmt=".2e"):
+        if self.is_mx_format:
+            return "None"
+        if self._use_constant_amax:
+            return f"{torch.finfo(torch.float8_e4m3fn).max:{fmt}}(const)"
+        if not hasattr(self, "_amax"):
+            return "dynamic"
+        if self._amax is None:
+            return "None"
+        if self._amax.is_meta:
+            return "meta"
+        return self._short_tensor(self._amax, fmt)
+
+    def _short_tensor(self, tensor: torch.Tensor, fmt=".2e"):
+        if tensor.numel() == 1:
+            return f"{tensor.item():{fmt}}"
+        return f"[{tensor.min().item():{fmt}}, {tensor.max().item():{fmt}}]({tensor.numel()})"
+
+    def extra_repr(self):
+        if self._disabled:
+            s = "disabled"
+            if self.pre_quant_scale is not None:
+                s += f" pre_quant_scale={self._short_tensor(self.pre_quant_scale)}"
+            return s
+        s = f"{'unsigned ' if self._unsigned else ''}{self._num_bits} bit"
+        s += " narrow" if self._narrow_range else ""
+        s += " fake" if self._fake_quant else ""
+        if self.block_sizes is not None:
+            s += f" block_sizes={self._block_sizes},"
+        else:
+            s += f" axis={self._axis}" if self._axis is not None else " per-tensor"
+        s += f" amax={self._short_amax()}"
+        if self.pre_quant_scale is not None:
+            s += f" pre_quant_scale={self._short_tensor(self.pre_quant_scale)}"
+        s += f" calibrator={self._calibrator.__class__.__name__}" if self._calibrator is not None else ""
+        s += " quant" if self._if_quant else ""
+        s += " calib" if self._if_calib else ""
+        if self.backend is not None:
+            s += f" backend={self.backend}, extra_args={self.backend_extra_args}"
+        return s
+
+    def _get_properties_for_modelopt_state(self):
+        return self.__dict__.keys() - nn.Module().__dict__.keys() - self._skip_properties_for_save_restore
+
+    def _get_pytorch_state_metadata(self):
+        metadata = {"params": {}, "buffers": {}}
+        for k, v in self._parameters.items():
+            metadata["params"][k] = {"shape": v.shape, "dtype": v.dtype}
+        for k, v in self._buffers.items():
+            if k in self._non_persistent_buffers_set:
+                continue
+            metadata["buffers"][k] = {"shape": v.shape, "dtype": v.dtype}
+        return metadata
+
+    def _reset_pytorch_state_from_metadata(self, metadata: dict[str, Any]):
+        self._parameters.clear()
+        self._buffers.clear()
+        self._non_persistent_buffers_set.clear()
+        for k, v in metadata.get("params", {}).items():
+            self.register_parameter(k, nn.Parameter(torch.empty(v["shape"], dtype=v.get("dtype"))))
+        for k, v in metadata.get("buffers", {}).items():
+            self.register_buffer(k, torch.empty(v["shape"], dtype=v.get("dtype")))
+
+    def get_modelopt_state(self, properties_only: bool = False) -> dict[str, Any]:
+        state = {k: getattr(self, k) for k in self._get_properties_for_modelopt_state()}
+        if properties_only:
+            return state
+        state["_pytorch_state_metadata"] = self._get_pytorch_state_metadata()
+        return state
+
+    def set_from_modelopt_state(self, modelopt_state, properties_only: bool = False):
+        for key in modelopt_state.keys() - self._skip_properties_for_save_restore:
+            if key == "_pytorch_state_metadata":
+                continue
+            setattr(self, key, modelopt_state[key])
+        for key in ["_num_bits", "_axis", "_unsigned"]:
+            setattr(self._calibrator, key, getattr(self, key))
+        if not properties_only:
+            self._reset_pytorch_state_from_metadata(modelopt_state.get("_pytorch_state_metadata", {}))
+
+    def sync_amax_across_distributed_group(self, parallel_group):
+        """all_reduce(MAX) of this quantizer's amax (reference :1373-1385).  ``max_calibrate``
+        instead packs every quantizer's amax into one buffer (model_calib.sync_amax_packed)."""
+        import torch.distributed as dist
+
+        if parallel_group.is_initialized() and getattr(self, "_amax", None) is not None:
+            try:
+                dist.all_reduce(self._amax, op=dist.ReduceOp.MAX, group=parallel_group.group)
+            except RuntimeError as e:
+                warnings.warn(f"Failed to synchronize amax: {e}")
+
+    @contextlib.contextmanager
+    def disable_pre_quant_scale(self):
+        was = self._enable_pre_quant_scale
+        self._enable_pre_quant_scale = False
+        try:
+            yield
+        finally:
+            self._enable_pre_quant_scale = was
+
+    def _set_buffer(self, key, value):
+        if hasattr(self, key):
+            setattr(self, key, value)
+        else:
+            self.register_buffer(key, value)
+
+
+class StaticBlockScaleQuantizer(TensorQuantizer):
+    """Static-block quantizer keeping fp32 per-block amax (reference :1484-1731).
+
+    The promotion after max calibration (core_utils.py:1077-1150) swaps INT static-block weight
+    quantizers to this class and keeps ``_amax`` in fp32.  The NVFP4 two-level scale path and LSQ
+    are outside the hot path."""
+
+    _lsq: bool = False
+    _quant_max_bound: float = 6.0
+
+    def _preserve_amax_in_fp32(self):
+        amax = getattr(self, "_amax", None)
+        if amax is not None and not isinstance(amax, nn.Parameter):
+            self._amax = amax.to(dtype=torch.float32)
+
+    def _amax_setter_helper(self, value):
+        super()._amax_setter_helper(value)
+        self._preserve_amax_in_fp32()
+
+    @classmethod
+    def from_tensor_quantizer(cls, tq: TensorQuantizer, global_amax=None) -> "StaticBlockScaleQuantizer":
+        if isinstance(tq, cls):
+            tq._preserve_amax_in_fp32()
+            return tq
+        if tq.is_nvfp4_static:
+            raise NotImplementedError("modelopt_amd: NVFP4 static block scales are a 'next' item")
+        tq.__class__ = cls
+        tq._is_static_block_scale_quantizer = True
+        tq._quant_max_bound = float(tq.maxbound)
+        tq._preserve_amax_in_fp32()
+        return tq
+
+    @property
+    def global_amax(self):
+        return getattr(self, "_global_amax", None)
+
+    def _apply(self, fn, recurse=True):
+        amax = getattr(self, "_amax", None)
+        module = super()._apply(fn, recurse=recurse)
+        self._preserve_amax_in_fp32()
+        if amax is not None and amax.device.type != "meta" and hasattr(self, "_amax"):
+            self._amax.data.copy_(amax.to(self._amax.device, torch.float32))
+        return module
+
+
+class SequentialQuantizer(nn.Sequential):
+    """Apply several TensorQuantizers in sequence (reference :1834-1892)."""
+
+    _delegated_properties = ["fake_quant", "is_enabled", "amax"]
+    _delegated_methods = ["reset_amax", "disable", "enable", "load_calib_amax", "load_calib_bias"]
+
+    def __init__(self, *quantizers: TensorQuantizer):
+        super().__init__(*quantizers)
+        assert all(isinstance(q, TensorQuantizer) for q in self), "All quantizers must be a TensorQuantizer."
+
+    def __getattr__(self, name):
+        if name in SequentialQuantizer._delegated_properties:
+            return getattr(self[0], name)
+        if name in SequentialQuantizer._delegated_methods:
+
+            def method_wrapper(*args, **kwargs):
+                outputs = [getattr(q, name)(*args, **kwargs) for q in self]
+                return outputs[-1]
+
+            return method_wrapper
+        return super().__getattr__(name)
+
+    def set_from_attribute_config(self, attributes):
+        if not isinstance(attributes, (list, tuple)):
+            attributes = [attributes] * len(self)
+        for attribute, quantizer in zip(attributes, self):
+            quantizer.set_from_attribute_config(attribute)
+
+    def get_modelopt_state(self) -> dict[str, Any]:
+        return {"num_quantizers": len(self), "is_sequential_quantizer": True}
+
+    @staticmethod
+    @contextlib.contextmanager
+    def convert_to_single_quantizer(model, indx: int = 0):
+        original: dict[nn.Module, list] = {}
+        for name, module in list(model.named_modules()):
+            if isinstance(module, SequentialQuantizer):
+                parent = model.get_submodule(name.rpartition(".")[0])
+                original.setdefault(parent, []).append((name.rpartition(".")[-1], module))
+                setattr(parent, name.rpartition(".")[-1], module[indx])
+        yield
+        for parent, lst in original.items():
+            for name, sq in lst:
+                setattr(parent, name, sq)

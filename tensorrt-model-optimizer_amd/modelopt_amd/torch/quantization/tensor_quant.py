@@ -1,0 +1,205 @@
+"""Fake-quant functionals over the MI355X-native ops (reference: tensor_quant.py).
+
+The autograd Functions keep the reference's names, argument order and straight-through-estimator
+backward (tensor_quant.py:279-568); their forward calls ``torch.ops.modelopt_amd.*`` (HIP kernels
+behind include/mtq_amd.h).  ``quantize_op`` / ``dynamic_block_quantize_op`` carry the reference's
+torch.library schemas (tensor_quant.py:222-276) in the ``modelopt_amd`` namespace.  There is no
+ATen fallback: a CPU tensor or a missing extension raises.
+"""
+
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+from modelopt_amd._ext import ops as _ops
+
+from .config import QuantizerAttributeConfig
+
+__all__ = [
+    "DynamicBlockQuantizationFunction",
+    "FakeTensorQuantFunction",
+    "ScaledE4M3Function",
+    "dynamic_block_quant",
+    "dynamic_block_quantize_op",
+    "e4m3_cast",
+    "fake_tensor_quant",
+    "fp8_fake_quant",
+    "mx_format_map",
+    "quantize_op",
+    "scaled_e4m3",
+]
+
+mx_format_map = {
+    (4, 3): "E4M3",
+    (5, 2): "E5M2",
+    (3, 2): "E3M2",
+    (2, 3): "E2M3",
+    8: "INT8",
+    (8, 0): "E8M0",
+    (2, 1): "E2M1",
+    (1, 2): "E1M2",
+    (0, 3): "E0M3",
+    (3, 0): "E3M0",
+}
+
+FORMAT_CODES = {
+    "E4M3": 0, "E5M2": 1, "INT8": 2, "E0M3": 3, "E1M2": 4, "E3M0": 5, "E2M1": 6, "E3M2": 7,
+    "E2M3": 8, "E8M0": 9,
+}
+
+
+def quantize_op(input, amax, num_bits=8, exponent_bits=0, unsigned=False, narrow_range=True):
+    """``tensorrt::quantize_op`` schema (tensor_quant.py:222-226) on the HIP kernels."""
+    return _ops().quantize_op(input, amax, num_bits, exponent_bits, unsigned, narrow_range)
+
+
+def dynamic_block_quantize_op(
+    input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
+):
+    """``tensorrt::dynamic_block_quantize_op`` schema (tensor_quant.py:227-231)."""
+    return _ops().dynamic_block_quantize_op(
+        input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
+    )
+
+
+def e4m3_cast(x):
+    """Unscaled e4m3 round trip (``_fp8_eager(x, None)``)."""
+    return _ops().e4m3_cast(x)
+
+
+def fp8_fake_quant(x, amax=None):
+    """FP8 e4m3 fake quant with optional amax (``fp8_eager`` semantics)."""
+    if amax is None:
+        return e4m3_cast(x)
+    return quantize_op(x, amax, 8, 4, False, False)
+
+
+# Predefined descriptors (tensor_quant.py:279-287)
+QUANT_DESC_8BIT_PER_TENSOR = QuantizerAttributeConfig(num_bits=8)
+QUANT_DESC_UNSIGNED_8BIT_PER_TENSOR = QuantizerAttributeConfig(num_bits=8, unsigned=True)
+QUANT_DESC_8BIT_LINEAR_WEIGHT_PER_ROW = QuantizerAttributeConfig(num_bits=8, axis=(0))
+
+
+# ---- backward: straight-through estimator with clipping (tensor_quant.py:290-316) ----------------
+
+
+def _fake_tensor_quant_backward(inputs, amax, grad_outputs):
+    if amax is None:
+        return grad_outputs
+    zero = grad_outputs.new_zeros(1)
+    return torch.where(inputs.abs() <= amax, grad_outputs, zero)
+
+
+def _fake_quant_backward_function(ctx, grad_outputs, num_args=1):
+    saved = ctx.saved_tensors
+    if len(saved) == 0:
+        return (grad_outputs,) + (None,) * (num_args - 1)
+    inputs, amax = saved
+    return (_fake_tensor_quant_backward(inputs, amax, grad_outputs),) + (None,) * (num_args - 1)
+
+
+def _save_for_backward_if_needed(ctx, pass_through_bwd, inputs, amax):
+    if not pass_through_bwd and amax is not None:
+        amax = (
+            amax
+            if isinstance(amax, torch.Tensor)
+            else torch.tensor(amax, device=inputs.device, dtype=inputs.dtype)
+        )
+        ctx.save_for_backward(inputs, amax)
+
+
+class FakeTensorQuantFunction(Function):
+    """INT-n fake quant (tensor_quant.py:319-399)."""
+
+    @staticmethod
+    def forward(
+        ctx,
+        inputs,
+        amax,
+        bias=None,
+        num_bits=8,
+        unsigned=False,
+        narrow_range=True,
+        trt_high_precision_dtype=None,
+        pass_through_bwd=False,
+        block_size=None,
+        axis=None,
+    ):
+        if bias is not None:
+            inputs = inputs - bias
+        _save_for_backward_if_needed(ctx, pass_through_bwd, inputs, amax)
+        if not isinstance(amax, torch.Tensor):
+            amax = torch.tensor(float(amax), device=inputs.device)
+        outputs = quantize_op(inputs, amax, num_bits, 0, unsigned, narrow_range)
+        if bias is not None:
+            outputs = outputs + bias
+        return outputs
+
+    @staticmethod
+    def backward(ctx, grad_outputs):
+        return _fake_quant_backward_function(ctx, grad_outputs, num_args=10)
+
+
+class ScaledE4M3Function(Function):
+    """FP8 e4m3 fake quant (tensor_quant.py:402-460)."""
+
+    @staticmethod
+    def forward(ctx, inputs, amax, bias, E, M, trt_high_precision_dtype=None, pass_through_bwd=False):  # noqa: N803
+        if E != 4 or M != 3:
+            raise NotImplementedError("Only support E=4 & M=3 for now.")
+        if bias is not None:
+            inputs = inputs - bias
+        _save_for_backward_if_needed(ctx, pass_through_bwd, inputs, amax)
+        outputs = fp8_fake_quant(inputs, amax)
+        if bias is not None:
+            outputs = outputs + bias
+        return outputs
+
+    @staticmethod
+    def backward(ctx, grad_outputs):
+        return _fake_quant_backward_function(ctx, grad_outputs, num_args=7)
+
+
+def _dynamic_block_quantize_forward(ctx, inputs, block_size, amax, num_bits, scale_bits, *_):
+    if isinstance(num_bits, int):
+        exponent_bits = 0  # MXINT8
+    else:
+        assert isinstance(num_bits, tuple) and len(num_bits) == 2
+        exponent_bits = num_bits[0]
+        num_bits = num_bits[0] + num_bits[1] + 1
+    assert isinstance(scale_bits, tuple) and len(scale_bits) == 2
+    scale_exponent_bits = scale_bits[0]
+    scale_num_bits = scale_bits[0] + scale_bits[1] + 1
+    return dynamic_block_quantize_op(
+        inputs, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
+    )
+
+
+class DynamicBlockQuantizationFunction(Function):
+    """Dynamic block (MX) fake quant (tensor_quant.py:497-568)."""
+
+    @staticmethod
+    def forward(
+        ctx,
+        inputs,
+        block_size,
+        amax,
+        bias,
+        num_bits,
+        scale_bits,
+        trt_high_precision_dtype=None,
+        onnx_quantizer_type="dynamic",
+        pass_through_bwd=True,
+    ):
+        _save_for_backward_if_needed(ctx, pass_through_bwd, inputs, amax)
+        return _dynamic_block_quantize_forward(ctx, inputs, block_size, amax, num_bits, scale_bits)
+
+    @staticmethod
+    def backward(ctx, grad_outputs):
+        return _fake_quant_backward_function(ctx, grad_outputs, num_args=9)
+
+
+fake_tensor_quant = FakeTensorQuantFunction.apply
+scaled_e4m3 = ScaledE4M3Function.apply
+dynamic_block_quant = DynamicBlockQuantizationFunction.apply

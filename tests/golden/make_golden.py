@@ -1,0 +1,372 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE on the CPU.
+
+Run in the survey container only (it needs /root/reference; the GPU box never runs this):
+
+    python tests/golden/make_golden.py
+
+How the reference is imported: the reference package is importable from /root/reference with
+three tiny import shims created under /tmp/mo_shim (outside both repositories): a
+``nvidia_modelopt-0.0.0.dist-info/METADATA`` so ``modelopt/__init__.py`` can read its version, and
+stub ``omegaconf`` / ``pulp`` modules that the reference imports at module load for features off
+the fake-quant path (robust_json, the LP searcher).  None of the code under test is stubbed.
+
+Outputs (small; committed):
+  tensor_quant.safetensors   INT `_tensor_quant`, FP8 `fp8_eager`, `reduce_amax` cases
+  quantizer.safetensors      TensorQuantizer calibrate+quant cases (per-tensor, axis, block, padding)
+  calib.safetensors/.json    MaxCalibrator / HistogramCalibrator (+ entropy / percentile amax)
+  mtq_linear.safetensors     C1: mtq.quantize(nn.Linear(1024,1024), INT8_DEFAULT_CFG)
+  llama_fp8.safetensors      C2 class: tiny LlamaForCausalLM FP8_DEFAULT_CFG PTQ (amax + logits)
+  awq.safetensors/.json      C3 class: awq_lite on a small MLP (best alpha/scale, weights, amax)
+  presets.json               the reference preset configs
+  mx_kat.json                the MX known-answer tables of test_quantize_mxformats_cuda.py (data)
+"""
+
+from __future__ import annotations
+
+import ast
+import json
+import os
+import sys
+from pathlib import Path
+
+OUT = Path(__file__).resolve().parent
+REF = Path(os.environ.get("MTQ_REFERENCE", "/root/reference"))
+SHIM = Path("/tmp/mo_shim")
+
+
+def _make_shim():
+    (SHIM / "nvidia_modelopt-0.0.0.dist-info").mkdir(parents=True, exist_ok=True)
+    (SHIM / "nvidia_modelopt-0.0.0.dist-info" / "METADATA").write_text(
+        "Metadata-Version: 2.1\nName: nvidia-modelopt\nVersion: 0.0.0\n"
+    )
+    (SHIM / "omegaconf").mkdir(exist_ok=True)
+    (SHIM / "omegaconf" / "__init__.py").write_text(
+        "class DictConfig(dict): pass\nclass ListConfig(list): pass\n"
+        "class OmegaConf:\n    @staticmethod\n    def to_container(x, *a, **k): return x\n"
+        "    @staticmethod\n    def create(x=None, *a, **k): return x\n"
+    )
+    (SHIM / "pulp").mkdir(exist_ok=True)
+    (SHIM / "pulp" / "__init__.py").write_text(
+        "class _Dummy:\n    def __init__(self, *a, **k): pass\ndef __getattr__(name): return _Dummy\n"
+    )
+    sys.path[:0] = [str(SHIM), str(REF)]
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+
+
+_make_shim()
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+from safetensors.torch import save_file as _save_file  # noqa: E402
+
+import modelopt.torch.quantization as mtq  # noqa: E402
+from modelopt.torch.quantization import tensor_quant as tq  # noqa: E402
+from modelopt.torch.quantization.calib import HistogramCalibrator, MaxCalibrator  # noqa: E402
+from modelopt.torch.quantization.config import QuantizerAttributeConfig  # noqa: E402
+from modelopt.torch.quantization.nn import TensorQuantizer  # noqa: E402
+from modelopt.torch.quantization.utils import reduce_amax  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def save_file(t, path):
+    _save_file({k: v.detach().clone().contiguous() for k, v in t.items()}, path)
+
+
+def edges(shape, dtype, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(shape, generator=g) * scale
+    f = x.view(-1)
+    k = max(1, f.numel() // 64)
+    f[:k] = torch.round(f[:k] * 8) / 8 + 0.5 / 8
+    f[k : 2 * k] = 0.0
+    f[2 * k : 3 * k] = -0.0
+    f[3 * k] = 7.5 * scale
+    return x.to(dtype)
+
+
+DT = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}
+
+
+def gen_tensor_quant():
+    t, meta = {}, []
+    for dn, dt in DT.items():
+        x = edges((64, 136), dt, seed=1)
+        g = torch.Generator().manual_seed(2)
+        amaxes = {
+            "tensor": torch.tensor(2.5),
+            "row": torch.rand(64, 1, generator=g) * 3 + 0.05,
+            "col": torch.rand(1, 136, generator=g) * 3 + 0.05,
+        }
+        amaxes["row"][3] = 0.0
+        amaxes["col"][0, 5] = 1e-30
+        t[f"x_{dn}"] = x.clone()
+        for an, a in amaxes.items():
+            t[f"amax_{dn}_{an}"] = a.clone()
+            for nb, u, nr in [(8, False, True), (8, False, False), (4, False, False), (4, True, False), (3, False, True)]:
+                xi = x.abs() if u else x
+                key = f"int_{dn}_{an}_b{nb}_u{int(u)}_n{int(nr)}"
+                t[key + "_y"] = tq._tensor_quant(xi, a, nb, u, nr).contiguous()
+                meta.append({"key": key, "x": f"x_{dn}", "abs": u, "amax": f"amax_{dn}_{an}",
+                             "num_bits": nb, "unsigned": u, "narrow_range": nr})
+            key = f"fp8_{dn}_{an}"
+            t[key + "_y"] = tq.fp8_eager(x * 3, a).contiguous()
+            meta.append({"key": key, "x": f"x_{dn}", "x_scale": 3.0, "amax": f"amax_{dn}_{an}", "fp8": True})
+        # block-128 view, FP8 and INT4
+        xb = edges((32, 256), dt, seed=3).view(-1, 128)
+        ab = xb.float().abs().amax(dim=1, keepdim=True)
+        t[f"blk_{dn}_x"], t[f"blk_{dn}_amax"] = xb.clone(), ab.clone()
+        t[f"fp8blk_{dn}_y"] = tq.fp8_eager(xb, ab).contiguous()
+        t[f"int4blk_{dn}_y"] = tq._tensor_quant(xb, ab, 4, False, False).contiguous()
+        # plain e4m3 cast (amax None)
+        t[f"fp8cast_{dn}_x"] = (x * 100).contiguous()
+        t[f"fp8cast_{dn}_y"] = tq.fp8_eager(x * 100, None).contiguous()
+        # reduce_amax
+        xr = edges((6, 40, 24), dt, seed=4, scale=2.0)
+        t[f"amax_{dn}_x"] = xr.contiguous()
+        for name, ax in [("all", None), ("a0", [0]), ("a2", [2]), ("a01", [0, 1]), ("a02", [0, 2]), ("a12", [1, 2])]:
+            t[f"amax_{dn}_{name}"] = reduce_amax(xr, axis=ax).contiguous()
+    # special values, fp32
+    sv = torch.tensor([448.0, 449.0, 463.99, 464.0, 465.0, 480.0, 1e9, 0.0, -0.0, 2.0**-9, 2.0**-10,
+                       1.5 * 2.0**-10, 3.0, -5.5, 1e-20, 6e4])
+    for a in [448.0, 3.0, 0.0, 1e-30]:
+        t[f"fp8sv_{a}_y"] = tq.fp8_eager(sv, torch.tensor(a))
+    t["fp8sv_x"] = sv
+    save_file({k: v.contiguous() for k, v in t.items()}, str(OUT / "tensor_quant.safetensors"))
+    (OUT / "tensor_quant.json").write_text(json.dumps(meta, indent=0))
+
+
+def gen_quantizer():
+    t = {}
+    torch.manual_seed(10)
+
+    def calib_then_quant(name, cfg, x, y=None):
+        q = TensorQuantizer(QuantizerAttributeConfig(**cfg))
+        q.enable_calib()
+        q.disable_quant()
+        q(x)
+        q.load_calib_amax()
+        q.disable_calib()
+        q.enable_quant()
+        out = q(x if y is None else y)
+        t[name + "_x"] = x.contiguous()
+        if y is not None:
+            t[name + "_y_in"] = y.contiguous()
+        t[name + "_amax"] = q.amax.contiguous()
+        t[name + "_out"] = out.contiguous()
+
+    for dn, dt in DT.items():
+        x = edges((48, 256), dt, seed=11)
+        y = edges((48, 256), dt, seed=12, scale=1.3)
+        calib_then_quant(f"q_{dn}_int8_tensor", {"num_bits": 8}, x, y)
+        calib_then_quant(f"q_{dn}_int8_axis0", {"num_bits": 8, "axis": 0}, x, y)
+        calib_then_quant(f"q_{dn}_int8_axism1", {"num_bits": 8, "axis": -1}, x, y)
+        calib_then_quant(f"q_{dn}_fp8_tensor", {"num_bits": (4, 3)}, x, y)
+        calib_then_quant(f"q_{dn}_int4_b128", {"num_bits": 4, "block_sizes": {-1: 128, "type": "static"}}, x)
+        calib_then_quant(f"q_{dn}_fp8_b128", {"num_bits": (4, 3), "block_sizes": {-1: 128}}, x)
+    # padding / multi-axis block cases (tensor_quantizer_common.py:480-583)
+    g = torch.Generator().manual_seed(13)
+    a = torch.randn(3, 4, 5, generator=g)
+    calib_then_quant("blk_simple_padding", {"num_bits": 8, "block_sizes": {-1: 2}}, a)
+    b = torch.randn(2, 6, 4, generator=g)
+    q = TensorQuantizer(QuantizerAttributeConfig(num_bits=8, block_sizes={-1: 2, 1: 3}))
+    t["blk_complex_x"], t["blk_complex_out"] = b, q(b)
+    c = torch.randn(2, 10, 5, generator=g)
+    calib_then_quant("blk_complex_padding", {"num_bits": 8, "block_sizes": {-1: 2, 1: 3}}, c)
+    # dynamic per-token FP8 (block_sizes {-1: None, type: dynamic})
+    d = torch.randn(4, 7, 64, generator=g)
+    q = TensorQuantizer(QuantizerAttributeConfig(num_bits=(4, 3), type="dynamic", block_sizes={-1: None, "type": "dynamic"}))
+    t["fp8_per_token_x"], t["fp8_per_token_out"] = d, q(d)
+    save_file(t, str(OUT / "quantizer.safetensors"))
+
+
+def gen_calib():
+    t, meta = {}, {}
+    g = torch.Generator().manual_seed(20)
+    xs = [torch.randn(32, 64, generator=g) * s for s in (1.0, 2.5, 0.7)]
+    for i, x in enumerate(xs):
+        t[f"batch{i}"] = x
+    for name, axis in [("none", None), ("a0", 0), ("a1", 1)]:
+        c = MaxCalibrator(8, axis, False)
+        for x in xs:
+            c.collect(x)
+        t[f"max_{name}"] = c.compute_amax().contiguous()
+    # histogram: growth on the second batch
+    h = HistogramCalibrator(8, None, False, num_bins=256)
+    for x in xs:
+        h.collect(x)
+    t["hist"] = h._calib_hist.clone()
+    t["hist_edges"] = h._calib_bin_edges.clone()
+    meta["hist_num_bins"] = h._num_bins
+    meta["entropy"] = float(h.compute_amax("entropy", start_bin=128))
+    meta["percentile_99"] = float(h.compute_amax("percentile", percentile=99.0))
+    meta["percentile_9999"] = float(h.compute_amax("percentile", percentile=99.99))
+    h2 = HistogramCalibrator(8, None, False, num_bins=2048, skip_zeros=True)
+    xz = xs[0].clone()
+    xz[:4] = 0
+    h2.collect(xz)
+    t["hist_skip_zeros"] = h2._calib_hist.clone()
+    t["hist_skip_zeros_x"] = xz
+    save_file(t, str(OUT / "calib.safetensors"))
+    (OUT / "calib.json").write_text(json.dumps(meta, indent=1))
+
+
+def gen_mtq_linear():
+    torch.manual_seed(30)
+    m = nn.Linear(1024, 1024)
+    w0 = {k: v.clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(31)
+    calib = [torch.randn(16, 1024, generator=g) for _ in range(4)]
+    test = torch.randn(8, 1024, generator=g)
+
+    def loop(model):
+        for c in calib:
+            model(c)
+
+    mtq.quantize(m, mtq.INT8_DEFAULT_CFG, loop)
+    t = {"weight": w0["weight"], "bias": w0["bias"], "test": test, "out": m(test).detach()}
+    for i, c in enumerate(calib):
+        t[f"calib{i}"] = c
+    t["input_amax"] = m.input_quantizer.amax.clone()
+    t["weight_amax"] = m.weight_quantizer.amax.clone()
+    save_file(t, str(OUT / "mtq_linear.safetensors"))
+
+
+def tiny_llama():
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    cfg = LlamaConfig(
+        hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=4,
+        num_key_value_heads=2, vocab_size=32, max_position_embeddings=64,
+    )
+    torch.manual_seed(40)
+    return LlamaForCausalLM(cfg).eval()
+
+
+def gen_llama_fp8():
+    model = tiny_llama()
+    sd = {k: v.clone().contiguous() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(41)
+    ids = torch.randint(0, 32, (4, 2, 16), generator=g)
+    test = torch.randint(0, 32, (2, 16), generator=g)
+
+    def loop(mm):
+        for b in ids:
+            mm(b)
+
+    mtq.quantize(model, mtq.FP8_DEFAULT_CFG, loop)
+    t = {f"sd.{k}": v for k, v in sd.items()}
+    t["calib_ids"] = ids
+    t["test_ids"] = test
+    t["logits"] = model(test).logits.detach()
+    for n, q in model.named_modules():
+        if isinstance(q, TensorQuantizer) and q.amax is not None:
+            t[f"amax.{n}"] = q.amax.clone().contiguous()
+    save_file(t, str(OUT / "llama_fp8.safetensors"))
+
+
+class _SimpleMLP(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 16), nn.ReLU(), nn.Linear(16, 16))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def gen_awq():
+    torch.manual_seed(50)
+    model = _SimpleMLP()
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(51)
+    data = [torch.randn(2, 16, generator=g) for _ in range(4)]
+    cfg = {
+        "quant_cfg": [
+            {"quantizer_name": "*", "enable": False},
+            {"quantizer_name": "*weight_quantizer", "cfg": {"num_bits": 4, "block_sizes": {-1: 8, "type": "static"}}},
+        ],
+        "algorithm": {"method": "awq_lite", "alpha_step": 0.1, "debug": True},
+    }
+
+    def loop(mm):
+        for d in data:
+            mm(d)
+
+    mtq.quantize(model, cfg, loop)
+    t = {f"sd.{k}": v for k, v in sd.items()}
+    for i, d in enumerate(data):
+        t[f"data{i}"] = d
+    meta = {}
+    for n, m in model.named_modules():
+        if hasattr(m, "awq_lite"):
+            t[f"best_scale.{n}"] = m.awq_lite.best_scale.clone()
+            t[f"weight.{n}"] = m.weight.detach().clone()
+            t[f"wamax.{n}"] = m.weight_quantizer.amax.clone()
+            t[f"pqs.{n}"] = m.input_quantizer.pre_quant_scale.clone()
+            meta[n] = {"best_alpha": m.awq_lite.best_alpha, "loss": {str(k): float(v) for k, v in m.awq_lite.loss.items()}}
+    test = torch.randn(3, 16, generator=g)
+    t["test"] = test
+    t["out"] = model(test).detach()
+    save_file(t, str(OUT / "awq.safetensors"))
+    (OUT / "awq.json").write_text(json.dumps(meta, indent=1))
+
+
+def gen_presets():
+    names = [
+        "INT8_DEFAULT_CFG", "INT8_WEIGHT_ONLY_CFG", "FP8_DEFAULT_CFG", "FP8_PER_CHANNEL_PER_TOKEN_CFG",
+        "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG", "INT4_BLOCKWISE_WEIGHT_ONLY_CFG", "INT4_AWQ_CFG",
+        "MXFP8_DEFAULT_CFG", "MXFP6_DEFAULT_CFG", "MXFP4_DEFAULT_CFG", "MXINT8_DEFAULT_CFG",
+        "W4A8_MXFP4_FP8_CFG", "MXFP4_MLP_WEIGHT_ONLY_CFG",
+    ]
+
+    def enc(o):
+        if isinstance(o, dict):
+            return {("__int__" + str(k)) if isinstance(k, int) else k: enc(v) for k, v in o.items()}
+        if isinstance(o, (list, tuple)):
+            return {"__tuple__": [enc(v) for v in o]} if isinstance(o, tuple) else [enc(v) for v in o]
+        return o
+
+    (OUT / "presets.json").write_text(json.dumps({n: enc(getattr(mtq, n)) for n in names}, indent=0))
+
+
+def gen_mx_kat():
+    """Extract the literal in/out tables of the reference MX known-answer tests (data only)."""
+    src = (REF / "tests/gpu/torch/quantization/test_quantize_mxformats_cuda.py").read_text()
+    tree = ast.parse(src)
+    kats = {}
+    for fn in tree.body:
+        if not isinstance(fn, ast.FunctionDef) or fn.name not in ("test_mxfp4", "test_mxfp6", "test_mxfp8", "test_mxint8"):
+            continue
+        tables, calls = [], []
+        for node in ast.walk(fn):
+            if isinstance(node, ast.Call) and getattr(node.func, "attr", "") == "tensor" and node.args:
+                try:
+                    tables.append((node.lineno, ast.literal_eval(node.args[0])))
+                except ValueError:
+                    pass
+            if isinstance(node, ast.Subscript) and getattr(getattr(node, "value", None), "id", "") == "mx_format_map":
+                calls.append((node.lineno, ast.literal_eval(node.slice)))
+        tables.sort()
+        calls.sort()
+        bs = None
+        for node in ast.walk(fn):
+            if isinstance(node, ast.Assign) and getattr(node.targets[0], "id", "") == "block_size":
+                bs = ast.literal_eval(node.value)
+        # element formats in call order (scale formats (8, 0) skipped)
+        fmts = [c for _, c in calls if c != (8, 0)]
+        kats[fn.name] = {
+            "block_size": bs,
+            "input": tables[0][1],
+            "outputs": [{"format": list(f) if isinstance(f, tuple) else f, "expected": tab} for f, (_, tab) in zip(fmts, tables[1:])],
+        }
+    (OUT / "mx_kat.json").write_text(json.dumps(kats))
+
+
+if __name__ == "__main__":
+    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "awq", "presets", "mx_kat"]
+    for s in steps:
+        print("generating", s, flush=True)
+        globals()["gen_" + s]()
+    print("done")

@@ -1,0 +1,79 @@
+"""The C-ABI library loads and exports every symbol include/mtq_amd.h declares; the torch op
+library registers the reference's op schemas.  No GPU compute (CPU container)."""
+
+import ctypes
+
+import pytest
+import torch
+
+from modelopt_amd import _ext
+from oracle import ref_ops as R
+
+
+def test_header_symbols_exported():
+    lib = _ext.kernel_cdll()
+    syms = _ext.declared_symbols()
+    assert len(syms) >= 12, syms
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_status_strings_and_version():
+    lib = _ext.kernel_cdll()
+    assert lib.mtq_status_string(0) == b"ok"
+    assert b"Blocksize" in lib.mtq_status_string(-3)
+    lib.mtq_version.restype = ctypes.c_int
+    assert lib.mtq_version() >= 100
+
+
+def test_invalid_args_rejected_without_gpu():
+    """Argument validation happens before any HIP call, so it runs here."""
+    lib = _ext.kernel_cdll()
+    f = lib.mtq_fused_amax_convert
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    fake = ctypes.c_void_p(256)  # never dereferenced: validation fails before any HIP call
+    assert f(fake, fake, 4, 64, 2, 64, 6, 9, None, 0, None) == -3  # block size
+    assert f(fake, fake, 4, 64, 2, 32, 11, 9, None, 0, None) == -4  # format
+    assert f(None, None, 4, 64, 2, 32, 6, 9, None, 0, None) == -1  # null pointers
+    g = lib.mtq_fake_tensor_quant
+    g.restype = ctypes.c_int
+    g.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    assert g(None, None, 16, 2, None, 0, 8, 0, 1, None) == -1
+    assert g(fake, fake, 16, 7, fake, 0, 8, 0, 1, None) == -2  # dtype
+
+
+@pytest.mark.parametrize("fmt", ["E2M1", "E3M2", "E2M3", "E4M3", "E5M2", "INT8", "E1M2", "E0M3", "E3M0"])
+def test_host_convert_to_exmy_matches_oracle(fmt):
+    """mtq_convert_to_exmy (the reference's `convert_to_exmy`) vs the oracle's table walk."""
+    lib = _ext.kernel_cdll()
+    g = torch.Generator().manual_seed(0)
+    xs = torch.cat([torch.randn(2000, generator=g) * s for s in (0.1, 1, 10, 1000)])
+    xs = torch.cat([xs, torch.tensor([0.0, -0.0, 0.25, 0.75, 5.0, 6.0, 7.0, 464.0, 465.0, 57344.0, 1e30])])
+    ref = R.convert_to_types(xs, fmt)
+    out = torch.tensor([lib.mtq_convert_to_exmy(float(v), R.FORMAT_CODES[fmt]) for v in xs.tolist()])
+    assert torch.equal(out, ref), (out - ref).abs().max()
+
+
+def test_op_library_registers_schemas():
+    ops = _ext.ops()
+    for name in ["quantize_op", "dynamic_block_quantize_op", "fake_tensor_quant", "fake_tensor_quant_",
+                 "fake_tensor_quant_with_axis", "fake_e4m3fy", "fake_e4m3fy_with_axis",
+                 "fused_amax_convert", "amax_accumulate", "block_quant_dynamic", "histogram_abs_accumulate"]:
+        assert hasattr(ops, name), name
+    schema = str(torch.ops.modelopt_amd.quantize_op.default._schema)
+    assert "int num_bits, int exponent_bits, bool unsigned, bool narrow_range" in schema
+
+
+def test_cpu_tensor_fails_loudly():
+    """No CPU compute path in the product: a CPU tensor raises instead of falling back."""
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        _ext.ops().quantize_op(torch.randn(4, 4), torch.tensor(1.0), 8, 0, False, True)
+
+
+def test_meta_kernels():
+    x = torch.empty(3, 5, device="meta", dtype=torch.bfloat16)
+    y = _ext.ops().quantize_op(x, torch.empty((), device="meta"), 8, 4, False, False)
+    assert y.shape == x.shape and y.dtype == x.dtype and y.device.type == "meta"

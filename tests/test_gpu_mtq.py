@@ -1,0 +1,132 @@
+"""End-to-end mtq.quantize on the GPU against the reference's CPU results (golden fixtures).
+
+C1 (nn.Linear(1024,1024) INT8_DEFAULT_CFG), the C2 model class (tiny LlamaForCausalLM,
+FP8_DEFAULT_CFG) and the C3 algorithm (awq_lite on a small MLP).  Weight-side amax is bit-exact
+(same data, exact max); activation amax and outputs go through GEMMs whose summation order differs
+between the reference's CPU run and hipBLASLt, so they are compared with a tolerance stated per test.
+"""
+
+from pathlib import Path
+
+import json
+
+import pytest
+import torch
+import torch.nn as nn
+from safetensors.torch import load_file
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+
+
+def test_c1_linear_int8(gpu):
+    import modelopt_amd.torch.quantization as mtq
+
+    t = load_file(str(G / "mtq_linear.safetensors"))
+    m = nn.Linear(1024, 1024).to(gpu)
+    m.load_state_dict({"weight": t["weight"], "bias": t["bias"]})
+    calib = [t[f"calib{i}"].to(gpu) for i in range(4)]
+
+    def loop(model):
+        for c in calib:
+            model(c)
+
+    mtq.quantize(m, mtq.INT8_DEFAULT_CFG, loop)
+    # activations of a single Linear are its inputs: amax exact on both sides
+    assert torch.equal(m.input_quantizer.amax.cpu(), t["input_amax"])
+    assert torch.equal(m.weight_quantizer.amax.cpu(), t["weight_amax"])
+    out = m(t["test"].to(gpu)).detach().cpu()
+    torch.testing.assert_close(out, t["out"], rtol=1e-5, atol=2e-5)  # fp32 GEMM order only
+
+
+def _tiny_llama():
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    cfg = LlamaConfig(hidden_size=32, intermediate_size=64, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=32, max_position_embeddings=64)
+    return LlamaForCausalLM(cfg).eval()
+
+
+def test_c2_tiny_llama_fp8(gpu):
+    import modelopt_amd.torch.quantization as mtq
+
+    t = load_file(str(G / "llama_fp8.safetensors"))
+    model = _tiny_llama()
+    model.load_state_dict({k[3:]: v for k, v in t.items() if k.startswith("sd.")})
+    model.to(gpu)
+    ids = t["calib_ids"].to(gpu)
+
+    def loop(mm):
+        for b in ids:
+            mm(b)
+
+    mtq.quantize(model, mtq.FP8_DEFAULT_CFG, loop)
+    got = {n: q.amax for n, q in model.named_modules() if isinstance(q, mtq.TensorQuantizer) and q.amax is not None}
+    want = {k[5:]: v for k, v in t.items() if k.startswith("amax.")}
+    assert set(got) == set(want)
+    for n, v in want.items():
+        if "weight_quantizer" in n:
+            assert torch.equal(got[n].cpu(), v), n
+        else:
+            torch.testing.assert_close(got[n].cpu(), v, rtol=1e-5, atol=1e-6)
+    logits = model(t["test_ids"].to(gpu)).logits.detach().cpu()
+    torch.testing.assert_close(logits, t["logits"], rtol=2e-3, atol=2e-3)
+
+
+class _SimpleMLP(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 16), nn.ReLU(), nn.Linear(16, 16))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def test_c3_awq_lite(gpu):
+    import modelopt_amd.torch.quantization as mtq
+
+    t = load_file(str(G / "awq.safetensors"))
+    meta = json.loads((G / "awq.json").read_text())
+    model = _SimpleMLP()
+    model.load_state_dict({k[3:]: v for k, v in t.items() if k.startswith("sd.")})
+    model.to(gpu)
+    data = [t[f"data{i}"].to(gpu) for i in range(4)]
+    cfg = {
+        "quant_cfg": [
+            {"quantizer_name": "*", "enable": False},
+            {"quantizer_name": "*weight_quantizer", "cfg": {"num_bits": 4, "block_sizes": {-1: 8, "type": "static"}}},
+        ],
+        "algorithm": {"method": "awq_lite", "alpha_step": 0.1, "debug": True},
+    }
+
+    def loop(mm):
+        for d in data:
+            mm(d)
+
+    mtq.quantize(model, cfg, loop)
+    for n, m in model.named_modules():
+        if not hasattr(m, "awq_lite"):
+            continue
+        assert m.awq_lite.best_alpha == pytest.approx(meta[n]["best_alpha"]), n
+        torch.testing.assert_close(m.awq_lite.best_scale.cpu(), t[f"best_scale.{n}"], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(m.weight.detach().cpu(), t[f"weight.{n}"], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(m.weight_quantizer.amax.cpu(), t[f"wamax.{n}"], rtol=1e-4, atol=1e-6)
+    out = model(t["test"].to(gpu)).detach().cpu()
+    torch.testing.assert_close(out, t["out"], rtol=1e-3, atol=1e-4)
+
+
+def test_weight_collect_once_per_version(gpu):
+    """A weight is reduced once per calibration even though forward_loop touches it every batch
+    (the reference re-reduces it per batch); an in-place update makes it collect again."""
+    from modelopt_amd.torch.quantization.calib import MaxCalibrator
+
+    c = MaxCalibrator()
+    w = nn.Parameter(torch.randn(64, 64, device=gpu))
+    c.collect(w)
+    a0 = c.compute_amax().clone()
+    c.collect(w)  # same object, same version: skipped (same result either way)
+    assert torch.equal(c.compute_amax(), a0)
+    with torch.no_grad():
+        w.mul_(2)
+    c.collect(w)
+    assert torch.equal(c.compute_amax(), a0 * 2)
