@@ -16,7 +16,8 @@ Also reported (same JSON line):
   kernels       per-kernel G-elem/s and % roofline for the other hot-path formats
   cpu_baseline  the oracle's restatement of the reference eager path (tensor_quant.py:46-59) timed
                 on this host's cores on a bounded sample (rank 0, N=1 only)
-  ptq           Llama-3-8B FP8 PTQ wall-clock (512 synthetic samples x 512 tokens) when --ptq
+  ptq           Llama-3-8B FP8 PTQ wall-clock (512 synthetic samples x 512 tokens; DP over ranks,
+                slowest rank), the bf16 forward of the same batches at N=1, and the difference
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
 """
@@ -185,7 +186,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-suite", action="store_true", help="skip the secondary kernel table")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
-    ap.add_argument("--ptq", action="store_true", help="also time Llama-3-8B FP8 PTQ (512 samples)")
+    ap.add_argument("--no-ptq", action="store_true", help="skip the Llama-3-8B FP8 PTQ wall-clock")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
@@ -245,10 +246,16 @@ def main():
     }
     if rank == 0 and not args.no_suite:
         out["kernels"] = kernel_suite(ops, xs, args.steps, args.warmup)
-    if rank == 0 and args.ptq:
+    if not args.no_ptq:
         from scripts import ptq_llama  # noqa: PLC0415
 
-        out["ptq"] = ptq_llama.run(samples=512, seq=512)
+        del xs, blk
+        torch.cuda.empty_cache()
+        _barrier(dist)
+        res = ptq_llama.run(samples=512, seq=512, rank=rank, world=world, baseline=(world == 1))
+        res["ptq_wall_clock_s"] = round(_max_over_ranks(dist, res["ptq_wall_clock_s"]), 3)
+        res["calib_tokens_per_s"] = round(512 * 512 / res["ptq_wall_clock_s"], 1)
+        out["ptq"] = res
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
