@@ -8,9 +8,10 @@ exact max, so order and fusion cannot change it); the differences are where the 
 * no host synchronisation in ``collect``: the reference's three NaN / negative / inf asserts
   (calib/max.py:69-77) are evaluated once, lazily, when the amax is read (``compute_amax``), and
   raise the same AssertionError messages there;
-* a second ``collect`` of the *same* tensor object at the same version (the weight of a
-  QuantLinear during ``forward_loop``, which the reference re-reduces on every batch) is skipped:
-  max(a, a) = a.
+* a second ``collect`` of the *same* data at the same version -- the same tensor object, or the
+  same view (offset/shape/stride) of the same live base tensor (the weight of a QuantLinear, or
+  one expert's slice of a fused [E, N, K] expert weight, during ``forward_loop``, which the
+  reference re-reduces on every batch) -- is skipped: max(a, a) = a.
 """
 
 from __future__ import annotations
@@ -36,18 +37,24 @@ class MaxCalibrator(_Calibrator):
         self._acc = None  # fp32 running max, flat
         self._out_shape = None
         self._out_dtype = None
-        self._last = None  # (weakref to the last collected tensor, its _version)
+        self._last = None  # (weakref to the base of the last collected tensor, view key, _version)
         self._meta_amax = None
 
     @property
     def amaxs(self):
         return self._amaxs
 
+    @staticmethod
+    def _view_key(x):
+        base = x._base if x._base is not None else x
+        return base, (x.storage_offset(), tuple(x.shape), x.stride(), x.dtype)
+
     def _same_as_last(self, x) -> bool:
         if self._last is None:
             return False
-        ref, ver = self._last
-        return ref() is x and x._version == ver
+        ref, key, ver = self._last
+        base, k = self._view_key(x)
+        return ref() is base and k == key and x._version == ver
 
     @torch.no_grad()
     def collect(self, x):
@@ -71,7 +78,8 @@ class MaxCalibrator(_Calibrator):
             raise RuntimeError("amax shape changed!")
         quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
         try:
-            self._last = (weakref.ref(x), x._version)
+            base, key = self._view_key(x)
+            self._last = (weakref.ref(base), key, x._version)
         except TypeError:
             self._last = None
         if self._track_amax:

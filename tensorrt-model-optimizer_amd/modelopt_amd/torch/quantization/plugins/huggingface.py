@@ -1,1 +1,121 @@
-"""HuggingFace plugins (filled in with the MoE fused-experts path)."""
+"""HuggingFace MoE plugins on the PTQ hot path (reference: plugins/huggingface.py).
+
+``_QuantFusedExperts`` (reference :976-1115) wraps transformers-5 fused expert containers
+(``gate_up_proj`` [E, 2I, H] + ``down_proj`` [E, H, I] 3-D parameters; Mixtral, Qwen-MoE, OLMoE,
+...): one shared input quantizer per projection and one weight quantizer per expert, applied by
+intercepting the two ``F.linear`` calls the HF eager expert loop makes per expert (the expert index
+is recovered from the weight slice's storage offset).  Registered on the fly for every module type
+with that structure (reference :1697-1720), so ``mtq.quantize`` on a Mixtral model needs no setup.
+"""
+
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.nn as nn
+
+from ..nn.modules.quant_module import QuantModule, QuantModuleRegistry
+from ..nn.modules.tensor_quantizer import TensorQuantizer
+from . import register_on_the_fly
+
+__all__ = ["_QuantFusedExperts", "register_fused_experts_on_the_fly"]
+
+
+@contextlib.contextmanager
+def _replace_function(package, name, new_fn):
+    old = getattr(package, name)
+    setattr(package, name, new_fn)
+    try:
+        yield
+    finally:
+        setattr(package, name, old)
+
+
+class _QuantFusedExperts(QuantModule):
+    _first_proj_attr = "gate_up_proj"
+
+    def _setup(self):
+        n = self.num_experts
+        setattr(self, f"{self._first_proj_attr}_input_quantizer", TensorQuantizer())
+        setattr(self, f"{self._first_proj_attr}_weight_quantizers", nn.ModuleList([TensorQuantizer() for _ in range(n)]))
+        self.down_proj_input_quantizer = TensorQuantizer()
+        self.down_proj_weight_quantizers = nn.ModuleList([TensorQuantizer() for _ in range(n)])
+        self.__dict__["_down_proj_linear"] = False
+        self.__dict__["_current_expert_idx"] = 0
+
+    def _get_expert_idx_from_first_proj(self, weight: torch.Tensor) -> int:
+        first = getattr(self, self._first_proj_attr)
+        stride = first.stride(0)
+        if stride == 0:
+            return 0
+        idx = (weight.storage_offset() - first.storage_offset()) // stride
+        assert 0 <= idx < self.num_experts, (
+            f"Computed expert index {idx} out of range [0, {self.num_experts}). "
+            "This can happen if the weight was .contiguous()-copied or redistributed."
+        )
+        return idx
+
+    def forward(self, *args, **kwargs):
+        orig_linear = torch.nn.functional.linear
+        first_in = getattr(self, f"{self._first_proj_attr}_input_quantizer")
+        first_w = getattr(self, f"{self._first_proj_attr}_weight_quantizers")
+
+        def _quantized_linear(input, weight, bias=None):
+            d = self.__dict__
+            if d["_down_proj_linear"]:
+                idx = d["_current_expert_idx"]
+                input = self.down_proj_input_quantizer(input)
+                weight = self.down_proj_weight_quantizers[idx](weight)
+            else:
+                idx = self._get_expert_idx_from_first_proj(weight)
+                d["_current_expert_idx"] = idx
+                input = first_in(input)
+                weight = first_w[idx](weight)
+            d["_down_proj_linear"] = not d["_down_proj_linear"]
+            return orig_linear(input, weight, bias)
+
+        self.__dict__["_down_proj_linear"] = False
+        with _replace_function(torch.nn.functional, "linear", _quantized_linear):
+            return self._original_cls.forward(self, *args, **kwargs)
+
+    def iter_weights_for_calibration(self):
+        for wname, qname in ((self._first_proj_attr, f"{self._first_proj_attr}_weight_quantizers"),
+                             ("down_proj", "down_proj_weight_quantizers")):
+            weight = getattr(self, wname, None)
+            qs = getattr(self, qname, None)
+            if weight is None or qs is None:
+                continue
+            for idx, q in enumerate(qs):
+                yield weight[idx], q
+
+    def fold_weight(self, keep_attrs: bool = False):
+        for w, q in self.iter_weights_for_calibration():
+            if isinstance(q, TensorQuantizer) and q.fake_quant:
+                self._fold_weight_quantizer(q, (w,), keep_attrs)
+
+
+def _fused_experts_wrapper_class(module):
+    if not hasattr(module, "num_experts"):
+        return None
+    down = getattr(module, "down_proj", None)
+    if not isinstance(down, torch.Tensor) or down.dim() != 3:
+        return None
+    gate_up = getattr(module, "gate_up_proj", None)
+    if isinstance(gate_up, torch.Tensor) and gate_up.dim() == 3:
+        return _QuantFusedExperts
+    return None
+
+
+@register_on_the_fly
+def register_fused_experts_on_the_fly(model):
+    """Register every fused-experts module type found in ``model`` (reference :1697-1720)."""
+    seen = set()
+    for _, module in model.named_modules():
+        t = type(module)
+        if t in seen or t in QuantModuleRegistry:
+            continue
+        seen.add(t)
+        cls = _fused_experts_wrapper_class(module)
+        if cls is not None:
+            QuantModuleRegistry.register({t: f"hf.{t.__name__}"})(cls)

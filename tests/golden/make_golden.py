@@ -267,6 +267,45 @@ def gen_llama_fp8():
     save_file(t, str(OUT / "llama_fp8.safetensors"))
 
 
+def tiny_mixtral():
+    from transformers import MixtralConfig, MixtralForCausalLM
+
+    cfg = MixtralConfig(
+        hidden_size=32, intermediate_size=48, num_hidden_layers=2, num_attention_heads=4,
+        num_key_value_heads=2, vocab_size=32, max_position_embeddings=64, num_local_experts=4,
+        num_experts_per_tok=2,
+    )
+    torch.manual_seed(60)
+    return MixtralForCausalLM(cfg).eval()
+
+
+def gen_mixtral_fp8():
+    """Fused-experts MoE path (plugins/huggingface.py _QuantFusedExperts) under FP8_DEFAULT_CFG."""
+    model = tiny_mixtral()
+    sd = {k: v.clone().contiguous() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(61)
+    ids = torch.randint(0, 32, (4, 2, 16), generator=g)
+    test = torch.randint(0, 32, (2, 16), generator=g)
+
+    def loop(mm):
+        for b in ids:
+            mm(b)
+
+    mtq.quantize(model, mtq.FP8_DEFAULT_CFG, loop)
+    t = {f"sd.{k}": v for k, v in sd.items()}
+    t["calib_ids"] = ids
+    t["test_ids"] = test
+    t["logits"] = model(test).logits.detach()
+    names = []
+    for n, q in model.named_modules():
+        if isinstance(q, TensorQuantizer):
+            names.append([n, bool(q.is_enabled)])
+            if q.amax is not None:
+                t[f"amax.{n}"] = q.amax.clone().contiguous()
+    save_file(t, str(OUT / "mixtral_fp8.safetensors"))
+    (OUT / "mixtral_fp8.json").write_text(json.dumps({"quantizers": names}, indent=0))
+
+
 class _SimpleMLP(nn.Module):
     def __init__(self):
         super().__init__()
@@ -365,7 +404,7 @@ def gen_mx_kat():
 
 
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "awq", "presets", "mx_kat"]
+    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "awq", "presets", "mx_kat"]
     for s in steps:
         print("generating", s, flush=True)
         globals()["gen_" + s]()

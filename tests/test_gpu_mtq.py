@@ -73,6 +73,43 @@ def test_c2_tiny_llama_fp8(gpu):
     torch.testing.assert_close(logits, t["logits"], rtol=2e-3, atol=2e-3)
 
 
+def _tiny_mixtral():
+    from transformers import MixtralConfig, MixtralForCausalLM
+
+    cfg = MixtralConfig(hidden_size=32, intermediate_size=48, num_hidden_layers=2, num_attention_heads=4,
+                        num_key_value_heads=2, vocab_size=32, max_position_embeddings=64,
+                        num_local_experts=4, num_experts_per_tok=2)
+    return MixtralForCausalLM(cfg).eval()
+
+
+def test_c5_tiny_mixtral_fp8_fused_experts(gpu):
+    """C5 model class: transformers-5 fused experts through _QuantFusedExperts.  Per-expert weight
+    amax bit-exact; activation amax / logits within the GEMM-order tolerance of test_c2."""
+    import modelopt_amd.torch.quantization as mtq
+
+    t = load_file(str(G / "mixtral_fp8.safetensors"))
+    model = _tiny_mixtral()
+    model.load_state_dict({k[3:]: v for k, v in t.items() if k.startswith("sd.")})
+    model.to(gpu)
+    ids = t["calib_ids"].to(gpu)
+
+    def loop(mm):
+        for b in ids:
+            mm(b)
+
+    mtq.quantize(model, mtq.FP8_DEFAULT_CFG, loop)
+    got = {n: q.amax for n, q in model.named_modules() if isinstance(q, mtq.TensorQuantizer) and q.amax is not None}
+    want = {k[5:]: v for k, v in t.items() if k.startswith("amax.")}
+    assert set(got) == set(want)
+    for n, v in want.items():
+        if "weight_quantizer" in n:
+            assert torch.equal(got[n].cpu(), v), n
+        else:
+            torch.testing.assert_close(got[n].cpu(), v, rtol=1e-5, atol=1e-6)
+    logits = model(t["test_ids"].to(gpu)).logits.detach().cpu()
+    torch.testing.assert_close(logits, t["logits"], rtol=2e-3, atol=2e-3)
+
+
 class _SimpleMLP(nn.Module):
     def __init__(self):
         super().__init__()
