@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""End-to-end PTQ wall-clock: mtq.quantize(Llama-3-8B, FP8_DEFAULT_CFG, 512 x 512 synthetic tokens).
+"""End-to-end PTQ wall-clock: mtq.quantize(Llama-3-8B | Mixtral-8x7B, FP8_DEFAULT_CFG, 512 x 512 tokens).
 
 SURVEY.md §8d (E2E): LlamaForCausalLM built from the Llama-3-8B config (random bf16 weights, no
 checkpoint -- there is no network), 512 samples x 512 token ids uniform in [0, 128256) (seed 1234),
@@ -8,7 +8,10 @@ torch.distributed initialised each rank calibrates samples/world (DP) and the am
 one packed all_reduce(MAX).  Also times the same forward passes without quantizers, so the
 quantizer overhead on top of the bf16 GEMMs is visible.
 
-    python scripts/ptq_llama.py [--layers 32] [--samples 512] [--seq 512] [--batch 16]
+C5 (``--model mixtral-8x7b``): Mixtral-8x7B dims (transformers-5 fused experts, 8 experts top-2,
+46.7 G params = 93 GB bf16, resident on one GPU), same calibration set (vocab 32000).
+
+    python scripts/ptq_llama.py [--model llama3-8b] [--layers 32] [--samples 512] [--seq 512] [--batch 16]
 """
 
 from __future__ import annotations
@@ -38,30 +41,52 @@ LLAMA3_8B = dict(
     rms_norm_eps=1e-5,
 )
 
+MIXTRAL_8X7B = dict(
+    hidden_size=4096,
+    intermediate_size=14336,
+    num_hidden_layers=32,
+    num_attention_heads=32,
+    num_key_value_heads=8,
+    vocab_size=32000,
+    max_position_embeddings=32768,
+    rope_theta=1e6,
+    rms_norm_eps=1e-5,
+    num_local_experts=8,
+    num_experts_per_tok=2,
+)
+MODELS = {"llama3-8b": ("Llama-3-8B", LLAMA3_8B), "mixtral-8x7b": ("Mixtral-8x7B", MIXTRAL_8X7B)}
 
-def build_model(layers: int, device):
-    from transformers import LlamaConfig, LlamaForCausalLM
 
-    cfg = LlamaConfig(**{**LLAMA3_8B, "num_hidden_layers": layers})
+def build_model(layers: int, device, model="llama3-8b"):
+    from transformers import LlamaConfig, LlamaForCausalLM, MixtralConfig, MixtralForCausalLM
+
+    dims = MODELS[model][1]
+    cfg_cls, model_cls = (MixtralConfig, MixtralForCausalLM) if model.startswith("mixtral") else (LlamaConfig, LlamaForCausalLM)
+    cfg = cfg_cls(**{**dims, "num_hidden_layers": layers})
     cfg._attn_implementation = "sdpa"
     torch.manual_seed(1234)
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.bfloat16)
     try:
         with torch.device(device):
-            model = LlamaForCausalLM(cfg)
+            model = model_cls(cfg)
     finally:
         torch.set_default_dtype(prev)
     return model.eval()
 
 
-def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", rank=0, world=1, baseline=True):
+def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", rank=0, world=1, baseline=True,
+        model_name="llama3-8b"):
     import modelopt_amd.torch.quantization as mtq
 
     dev = torch.device("cuda", torch.cuda.current_device())
-    model = build_model(layers, dev)
+    model = build_model(layers, dev, model_name)
+    if model_name.startswith("mixtral"):
+        # the bf16 baseline runs the same eager expert loop the quantized experts intercept
+        model.config._experts_implementation = "eager"
+    label, dims = MODELS[model_name]
     g = torch.Generator(device=dev).manual_seed(1234)
-    ids = torch.randint(0, LLAMA3_8B["vocab_size"], (samples, seq), device=dev, generator=g)
+    ids = torch.randint(0, dims["vocab_size"], (samples, seq), device=dev, generator=g)
     per = samples // world
     mine = ids[rank * per : (rank + 1) * per]
     batches = list(mine.split(batch))
@@ -71,7 +96,7 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
             for b in batches:
                 m(b)
 
-    res = {"model": f"Llama-3-8B dims, {layers} layers, bf16 random init", "samples": samples,
+    res = {"model": f"{label} dims, {layers} layers, bf16 random init", "samples": samples,
            "seq": seq, "batch": batch, "world": world, "config": config}
     if baseline:
         forward_loop(model)  # warm-up (kernels, allocator)
@@ -102,6 +127,7 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b", choices=sorted(MODELS))
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--samples", type=int, default=512)
     ap.add_argument("--seq", type=int, default=512)
@@ -109,4 +135,5 @@ if __name__ == "__main__":
     ap.add_argument("--config", default="FP8_DEFAULT_CFG")
     ap.add_argument("--no-baseline", action="store_true")
     a = ap.parse_args()
-    print(json.dumps(run(a.samples, a.seq, a.batch, a.layers, a.config, baseline=not a.no_baseline)), flush=True)
+    print(json.dumps(run(a.samples, a.seq, a.batch, a.layers, a.config, baseline=not a.no_baseline,
+                         model_name=a.model)), flush=True)

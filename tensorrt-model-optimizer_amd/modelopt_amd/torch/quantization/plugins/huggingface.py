@@ -19,7 +19,7 @@ from ..nn.modules.quant_module import QuantModule, QuantModuleRegistry
 from ..nn.modules.tensor_quantizer import TensorQuantizer
 from . import register_on_the_fly
 
-__all__ = ["_QuantFusedExperts", "register_fused_experts_on_the_fly"]
+__all__ = ["_QuantFusedExperts", "force_eager_experts_impl_on_the_fly", "register_fused_experts_on_the_fly"]
 
 
 @contextlib.contextmanager
@@ -95,6 +95,10 @@ class _QuantFusedExperts(QuantModule):
                 self._fold_weight_quantizer(q, (w,), keep_attrs)
 
 
+def _is_fused_experts_module(module) -> bool:
+    return _fused_experts_wrapper_class(module) is not None
+
+
 def _fused_experts_wrapper_class(module):
     if not hasattr(module, "num_experts"):
         return None
@@ -119,3 +123,26 @@ def register_fused_experts_on_the_fly(model):
         cls = _fused_experts_wrapper_class(module)
         if cls is not None:
             QuantModuleRegistry.register({t: f"hf.{t.__name__}"})(cls)
+
+
+@register_on_the_fly
+def force_eager_experts_impl_on_the_fly(model):
+    """Pin HF fused experts to the eager ``F.linear`` loop (reference :1725-1753).
+
+    transformers >= 5 dispatches ``@use_experts_implementation`` forwards on
+    ``config._experts_implementation`` (``grouped_mm`` / ``batched_mm`` on GPU), which never calls
+    ``F.linear`` and would silently bypass the expert quantizers.
+    """
+    if not any(_is_fused_experts_module(m) for m in model.modules()):
+        return
+
+    def _force(cfg):
+        if cfg is None:
+            return
+        if hasattr(cfg, "_experts_implementation"):
+            cfg._experts_implementation = "eager"
+        for sub in ("text_config", "vision_config", "audio_config", "speech_config"):
+            if hasattr(cfg, sub):
+                _force(getattr(cfg, sub))
+
+    _force(getattr(model, "config", None))

@@ -144,7 +144,9 @@ def test_fused_experts_conversion_matches_reference():
     want_enabled = {n for n, e in ref if e}
     want_all = {n for n, _ in ref if "embed_tokens" not in n and "_bmm_quantizer" not in n}
     m = _tiny_mixtral()
+    m.config._experts_implementation = "grouped_mm"
     mtq.conversion.replace_quant_module(m)
+    assert m.config._experts_implementation == "eager"  # grouped_mm would bypass F.linear
     mtq.set_quantizer_by_cfg(m, mtq.FP8_DEFAULT_CFG["quant_cfg"])
     got = {n: q.is_enabled for n, q in m.named_modules() if isinstance(q, TensorQuantizer)}
     assert set(got) == want_all
