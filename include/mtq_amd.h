@@ -146,6 +146,24 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
 int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                       int skip_zeros, uint32_t *counts, hipStream_t stream);
 
+/* ---- AWQ-lite search helpers ---------------------------------------------------------------
+ * loss[0] += mean(float(T(a - b))^2) over n elements of dtype T: the per-alpha search loss
+ * `(out - out_act).float().pow(2).mean()` (model_calib.py:1555) in one read of a and b
+ * (reference: 4 ATen passes with an fp32 intermediate).  The difference is rounded to T before
+ * squaring as the reference's T-typed subtraction does; the sum is fp32 per lane, double across
+ * blocks, and deterministic for a given n on a given device (fixed grid, fixed final order).
+ * `workspace` holds mtq_mse_workspace_floats(n, dtype) floats, zero-filled once before first
+ * use (the kernel leaves it reusable); one workspace per concurrently used stream. */
+int64_t mtq_mse_workspace_floats(int64_t n, int dtype);
+int mtq_mse_accumulate(const void *a, const void *b, int64_t n, int dtype, float *loss,
+                       float *workspace, int64_t workspace_floats, hipStream_t stream);
+
+/* y[r, c] = T(x[r, c] * scale[c]) -- the input side of the AWQ-lite search, `inputs *
+ * pre_quant_scale` (tensor_quantizer.py:1143-1144 via model_calib.py:1547); x, y [rows, cols]
+ * contiguous, scale [cols], all of dtype T; cols a multiple of 16 B / sizeof(T). */
+int mtq_mul_cols(const void *x, const void *scale, void *y, int64_t rows, int64_t cols, int dtype,
+                 hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -488,13 +488,25 @@ __device__ __forceinline__ uint32_t vec_absmax_bits(const Vec<T> &v) {
   return m;
 }
 
-// Per-tensor (K = 1, Q = 1): grid-stride vector loop, wave max, block max in LDS, one
+// Per-tensor (K = 1, Q = 1), grid-stride form (variant 1): wave max, block max in LDS, one
 // atomicMax per block on the fp32 bit pattern.
+__device__ __forceinline__ void block_atomic_max(uint32_t m, uint32_t *out) {
+  __shared__ uint32_t red[kThreads / 64];
+  m = wave_max_u32(m);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 1; k < kThreads / 64; ++k) m = red[k] > m ? red[k] : m;
+    atomicMax(out, m);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void amax_all_kernel(const T *__restrict__ x, int64_t n,
                                                              int64_t nvec, uint32_t *out) {
   using V = Vec<T>;
-  __shared__ uint32_t red[kThreads / 64];
   uint32_t m = 0;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride) {
@@ -506,15 +518,62 @@ __global__ __launch_bounds__(kThreads) void amax_all_kernel(const T *__restrict_
     uint32_t b = abs_bits_t<T>(x[t]);
     m = b > m ? b : m;
   }
-  m = wave_max_u32(m);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
+  block_atomic_max(m, out);
+}
+
+// Per-tensor, chunked form (default): block b owns vectors [b*256*U, (b+1)*256*U); every lane
+// issues its U non-temporal 16 B loads before reducing any of them (U loads in flight per lane,
+// no loop-carried address math), then one atomicMax per block.  The n % N scalar tail is folded
+// into the last block.
+template <typename T, int U>
+__global__ __launch_bounds__(kThreads) void amax_chunk_kernel(const T *__restrict__ x, int64_t n,
+                                                               int64_t nvec, uint32_t *out) {
+  using V = Vec<T>;
+  const int64_t base = (int64_t)blockIdx.x * kThreads * U + threadIdx.x;
+  uint32_t m = 0;
+  if (base + (int64_t)(U - 1) * kThreads < nvec) {
+    V v[U];
 #pragma unroll
-    for (int k = 1; k < kThreads / 64; ++k) m = red[k] > m ? red[k] : m;
-    atomicMax(out, m);
+    for (int u = 0; u < U; ++u) v[u] = ldg_vec_nt(x + (base + (int64_t)u * kThreads) * V::N);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t b = vec_absmax_bits(v[u]);
+      m = b > m ? b : m;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + (int64_t)u * kThreads;
+      if (i < nvec) {
+        uint32_t b = vec_absmax_bits(ldg_vec_nt(x + i * V::N));
+        m = b > m ? b : m;
+      }
+    }
   }
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int64_t t = nvec * V::N + threadIdx.x; t < n; t += kThreads) {
+      uint32_t b = abs_bits_t<T>(x[t]);
+      m = b > m ? b : m;
+    }
+  }
+  block_atomic_max(m, out);
+}
+
+int amax_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("MTQ_AMD_AMAX_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+template <typename T, int U>
+int launch_amax_chunk(const T *x, int64_t n, int64_t nvec, uint32_t *out, hipStream_t stream) {
+  int64_t blocks = (nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U);
+  if (blocks < 1) blocks = 1;
+  amax_chunk_kernel<T, U><<<(unsigned)blocks, kThreads, 0, stream>>>(x, n, nvec, out);
+  return check_launch();
 }
 
 // Rows: x viewed as [R, Q] contiguous rows (R = P*K), out[r % K].  G lanes per row (G = 64
@@ -602,9 +661,19 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
   const bool al = aligned16(x);
   if (K == 1 && (Q == 1 || P == 1)) {  // per-tensor
     int64_t nvec = al ? n / N : 0;
-    unsigned g = grid_for(n / N + 1, kThreads * 4);
-    amax_all_kernel<T><<<g, kThreads, 0, stream>>>(x, n, nvec, out);
-    return check_launch();
+    switch (al ? amax_variant() : 1) {  // unaligned: all-scalar grid-stride form
+    case 1: {
+      unsigned g = grid_for(n / N + 1, kThreads * 4);
+      amax_all_kernel<T><<<g, kThreads, 0, stream>>>(x, n, nvec, out);
+      return check_launch();
+    }
+    case 2:
+      return launch_amax_chunk<T, 4>(x, n, nvec, out, stream);
+    case 3:
+      return launch_amax_chunk<T, 16>(x, n, nvec, out, stream);
+    default:
+      return launch_amax_chunk<T, 8>(x, n, nvec, out, stream);
+    }
   }
   if (Q % N == 0 && al && Q >= N) {
     const int64_t R = P * K, qvec = Q / N;
@@ -745,6 +814,110 @@ __global__ __launch_bounds__(kThreads) void hist_vec_kernel(const T *__restrict_
   __syncthreads();
   for (int b = threadIdx.x; b < bins; b += kThreads)
     if (sh[b]) atomicAdd(counts + b, sh[b]);
+}
+
+
+// ============================================================================================
+// AWQ-lite search helpers: column scale (x * s[col]) and the per-alpha MSE loss
+// ============================================================================================
+// y = T(x * s[col]) -- the reference's `inputs * pre_quant_scale` (fp32 product, one rounding).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void mul_cols_kernel(const T *__restrict__ x,
+                                                             const T *__restrict__ sc,
+                                                             T *__restrict__ y, int64_t nvec,
+                                                             int64_t cols) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  const int64_t c0 = (i * N) % cols;  // cols % N == 0: a vector never straddles rows
+  V s = ldg_vec(sc + c0);
+#pragma unroll
+  for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(Elem<T>::ld(v.e[j]) * Elem<T>::ld(s.e[j]));
+  stg_vec_nt(y + i * N, v);
+}
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// loss[0] += sum(float(T(a - b))^2) / n -- `(out - out_act).float().pow(2).mean()`
+// (model_calib.py:1555) in one read of a and b.  Deterministic: fixed grid for a given n, each
+// block stores its partial, the last block to finish (agent-scope counter) sums the partials
+// in block order in double and resets the counter for the next call.
+constexpr int kMseU = 4;
+template <typename T>
+__global__ __launch_bounds__(kThreads) void mse_kernel(const T *__restrict__ a,
+                                                        const T *__restrict__ b, int64_t n,
+                                                        int64_t nvec, float *partials,
+                                                        unsigned *counter, float *loss) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  float acc = 0.f;
+  const int64_t chunk = (int64_t)kThreads * kMseU;
+  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < nvec; c0 += (int64_t)gridDim.x * chunk) {
+    V va[kMseU], vb[kMseU];
+#pragma unroll
+    for (int u = 0; u < kMseU; ++u) {
+      const int64_t i = c0 + u * kThreads + threadIdx.x;
+      if (i < nvec) {
+        va[u] = ldg_vec_nt(a + i * N);
+        vb[u] = ldg_vec_nt(b + i * N);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kMseU; ++u) {
+      const int64_t i = c0 + u * kThreads + threadIdx.x;
+      if (i < nvec) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          float d = Elem<T>::ld(Elem<T>::st(Elem<T>::ld(va[u].e[j]) - Elem<T>::ld(vb[u].e[j])));
+          acc += d * d;
+        }
+      }
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int64_t t = nvec * N + threadIdx.x; t < n; t += kThreads) {
+      float d = Elem<T>::ld(Elem<T>::st(Elem<T>::ld(a[t]) - Elem<T>::ld(b[t])));
+      acc += d * d;
+    }
+  }
+  __shared__ float red[kThreads / 64];
+  __shared__ bool last;
+  acc = wave_sum_f(acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bs = 0.f;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) bs += red[k];
+    __hip_atomic_store(partials + blockIdx.x, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = done == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (unsigned k = 0; k < gridDim.x; ++k)
+      tot += (double)__hip_atomic_load(partials + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    loss[0] += (float)(tot / (double)n);
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+int64_t mse_grid(int64_t n, int dtype) {
+  const int N = dtype == MTQ_F32 ? 4 : 8;
+  int64_t blocks = (n / N + (int64_t)kThreads * kMseU - 1) / ((int64_t)kThreads * kMseU);
+  const int64_t cap = (int64_t)num_cus() * 4;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  return blocks;
 }
 
 }  // namespace
@@ -926,6 +1099,48 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
       hist_kernel<T><<<g, kThreads, shm, stream>>>(xt, n, hmax, bins, skip_zeros, counts,
                                                    lds ? 1 : 0);
     }
+    return check_launch();
+  });
+}
+
+int64_t mtq_mse_workspace_floats(int64_t n, int dtype) {
+  if (n < 0 || (dtype != MTQ_F32 && dtype != MTQ_F16 && dtype != MTQ_BF16)) return -1;
+  return mse_grid(n, dtype) + 1;
+}
+
+int mtq_mse_accumulate(const void *a, const void *b, int64_t n, int dtype, float *loss,
+                       float *workspace, int64_t workspace_floats, hipStream_t stream) {
+  if (n < 0 || !loss || !workspace || (n > 0 && (!a || !b))) return MTQ_ERR_INVALID_ARG;
+  if (n == 0) return MTQ_OK;  // mean over nothing: the caller's torch path decides NaN
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    const int64_t grid = mse_grid(n, dtype);
+    if (workspace_floats < grid + 1) return MTQ_ERR_INVALID_ARG;
+    const bool al = aligned16(a) && aligned16(b);
+    const int64_t nvec = al ? n / N : 0;
+    if (!al && n > (int64_t)kThreads * 4096) return MTQ_ERR_INVALID_ARG;  // scalar path is tail-only
+    mse_kernel<T><<<(unsigned)grid, kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(a), reinterpret_cast<const T *>(b), n, nvec, workspace,
+        reinterpret_cast<unsigned *>(workspace + grid), loss);
+    return check_launch();
+  });
+}
+
+int mtq_mul_cols(const void *x, const void *scale, void *y, int64_t rows, int64_t cols, int dtype,
+                 hipStream_t stream) {
+  if (rows < 0 || cols < 1) return MTQ_ERR_INVALID_ARG;
+  if (rows == 0) return MTQ_OK;
+  if (!x || !scale || !y) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    if (cols % N != 0 || !aligned16(x) || !aligned16(y) || !aligned16(scale))
+      return MTQ_ERR_INVALID_ARG;
+    const int64_t nvec = rows * cols / N;
+    mul_cols_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), reinterpret_cast<const T *>(scale),
+        reinterpret_cast<T *>(y), nvec, cols);
     return check_launch();
   });
 }

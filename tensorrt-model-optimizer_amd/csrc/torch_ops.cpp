@@ -13,6 +13,9 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "mtq_amd.h"
@@ -286,6 +289,58 @@ void amax_accumulate(const at::Tensor &inputs, at::Tensor out, int64_t P, int64_
   check_status(st, "reduce_amax");
 }
 
+// Persistent zero-initialised workspace per (device, stream) for the deterministic MSE
+// reduction; the kernel restores its counter, so the buffer is filled once.
+at::Tensor mse_workspace(const at::Tensor &like, int64_t floats) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_pair((int)like.device().index(), cur_stream(like));
+  auto it = cache.find(key);
+  if (it == cache.end() || it->second.numel() < floats) {
+    at::Tensor w = at::zeros({std::max<int64_t>(floats, 4096)}, like.options().dtype(at::kFloat));
+    cache[key] = w;
+    return w;
+  }
+  return it->second;
+}
+
+void mse_accumulate(const at::Tensor &a, const at::Tensor &b, at::Tensor loss, int64_t index) {
+  check_device(a, "a");
+  check_device(b, "b");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.sizes() == b.sizes(),
+              "mse_accumulate: a and b must have the same dtype and shape");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.is_contiguous() && index >= 0 &&
+                  index < loss.numel(),
+              "mse_accumulate: loss must be a contiguous fp32 tensor and index in range");
+  const int dt = checked_dtype(a, "a");
+  TORCH_CHECK(dt != MTQ_F64, "mse_accumulate: float64 is not supported");
+  at::Tensor ac = a.contiguous(), bc = b.contiguous();
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(a.device());
+  const int64_t n = ac.numel();
+  const int64_t wf = mtq_mse_workspace_floats(n, dt);
+  at::Tensor ws = mse_workspace(ac, wf);
+  int st = mtq_mse_accumulate(ac.data_ptr(), bc.data_ptr(), n, dt, loss.data_ptr<float>() + index,
+                              ws.data_ptr<float>(), ws.numel(), cur_stream(ac));
+  check_status(st, "mse_accumulate");
+}
+
+at::Tensor mul_cols(const at::Tensor &x, const at::Tensor &scale) {
+  check_device(x, "inputs");
+  const int dt = checked_dtype(x, "inputs");
+  TORCH_CHECK(dt != MTQ_F64, "mul_cols: float64 is not supported");
+  at::Tensor xc = x.contiguous();
+  const int64_t cols = xc.size(-1);
+  at::Tensor s = scale.to(x.device(), x.scalar_type()).contiguous();
+  TORCH_CHECK(s.numel() == cols, "mul_cols: scale must have size(-1) elements");
+  at::Tensor y = at::empty_like(xc);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_mul_cols(xc.data_ptr(), s.data_ptr(), y.data_ptr(), xc.numel() / cols, cols, dt,
+                        cur_stream(xc));
+  check_status(st, "mul_cols");
+  return y;
+}
+
 at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at::Tensor> &pqs,
                                int64_t block, int64_t num_bits, bool is_unsigned,
                                bool narrow_range) {
@@ -397,6 +452,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "bool unsigned, bool narrow_range) -> Tensor");
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
         "bool skip_zeros) -> ()");
+  m.def("mse_accumulate(Tensor a, Tensor b, Tensor(a!) loss, int index) -> ()");
+  m.def("mul_cols(Tensor inputs, Tensor scale) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
@@ -412,6 +469,8 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("amax_accumulate", &amax_accumulate);
   m.impl("block_quant_dynamic", &block_quant_dynamic);
   m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);
+  m.impl("mse_accumulate", &mse_accumulate);
+  m.impl("mul_cols", &mul_cols);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
@@ -439,4 +498,6 @@ TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
          [](const at::Tensor &x, const c10::optional<at::Tensor> &, int64_t, int64_t, bool, bool) {
            return meta_like(x);
          });
+  m.impl("mul_cols", [](const at::Tensor &x, const at::Tensor &) { return meta_like(x); });
+  m.impl("mse_accumulate", [](const at::Tensor &, const at::Tensor &, at::Tensor, int64_t) {});
 }

@@ -312,6 +312,17 @@ def _weight_qdq_fast_path(wq: TensorQuantizer, weight: torch.Tensor):
     ), blk
 
 
+_FAST_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
+
+
+def _mse_fast(out, ref) -> bool:
+    return (
+        isinstance(out, torch.Tensor) and isinstance(ref, torch.Tensor) and out.is_cuda
+        and out.dtype == ref.dtype and out.dtype in _FAST_DTYPES and out.shape == ref.shape
+        and out.numel() > 0
+    )
+
+
 def _awq_forward(self, input, *args, **kwargs):
     """Patched QuantLinear forward during AWQ-lite (reference :1513-1560)."""
     helper = self.awq_lite
@@ -337,25 +348,34 @@ def _awq_forward(self, input, *args, **kwargs):
 
     fast, blk = _weight_qdq_fast_path(self.weight_quantizer, self.weight)
     out_act = out_actual[0] if isinstance(out_actual, tuple) else out_actual
+    ops = _ops()
+    x_fast = (
+        input.is_cuda and input.dtype == self.weight.dtype and input.dtype in _FAST_DTYPES
+        and input.shape[-1] % (16 // input.element_size()) == 0
+    )
     for ai, alpha in enumerate(helper.alphas):
         awq_scale = get_scale(helper.act_scale, helper.weight_scale, alpha, None)
         pqs_in = (1 / awq_scale).to(self.weight.dtype)
         pqs_w = awq_scale.to(self.weight.dtype)
         if fast and not args and not kwargs and type(self)._original_cls is nn.Linear:
             # fused: qdq(W * s) in one HIP pass, x * (1/s) as the input quantizer would apply it
-            wq = _ops().block_quant_dynamic(
+            wq = ops.block_quant_dynamic(
                 self.weight.detach(), pqs_w, blk, self.weight_quantizer._num_bits,
                 self.weight_quantizer._unsigned, self.weight_quantizer._narrow_range,
             )
-            xin = self.input_quantizer(input * pqs_in)
-            out = F.linear(xin, wq, self.bias)
+            xs = ops.mul_cols(input, pqs_in) if x_fast else input * pqs_in
+            out = F.linear(self.input_quantizer(xs), wq, self.bias)
             out = self.output_quantizer(out)
         else:
             self.input_quantizer.pre_quant_scale = pqs_in
             self.weight_quantizer.pre_quant_scale = pqs_w
             out = self._forward_no_awq(input, *args, **kwargs)
         out = out[0] if isinstance(out, tuple) else out
-        helper.loss[ai] += (out - out_act).float().pow(2).mean()
+        if _mse_fast(out, out_act):
+            # (out - out_act).float().pow(2).mean() in one HIP pass (model_calib.py:1494)
+            ops.mse_accumulate(out, out_act, helper.loss, ai)
+        else:
+            helper.loss[ai] += (out - out_act).float().pow(2).mean()
     helper.num_search_steps += 1
     return out_actual
 

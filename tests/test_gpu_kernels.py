@@ -329,3 +329,50 @@ def test_block_quant_dynamic(gpu, dtype, with_pqs):
     ref = R.int_block_qdq_dynamic(w, 128, 4, pqs)
     out = ops().block_quant_dynamic(w.to(gpu), None if pqs is None else pqs.to(gpu), 128, 4, False, False)
     assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_reduce_amax_unaligned_and_chunk_edges(gpu):
+    """Per-tensor amax: 16 B-misaligned views (scalar path) and sizes around the chunk size."""
+    from modelopt_amd.torch.quantization.utils.core_utils import reduce_amax
+
+    g = torch.Generator().manual_seed(7)
+    for n in [1, 7, 8, 2047, 2048 * 8, 2048 * 8 + 1, 3 * 2048 * 8 - 9, 1 << 21]:
+        base = torch.randn(n + 1, generator=g).to(torch.bfloat16)
+        for x in (base[:n], base[1:]):
+            ref = R.reduce_amax(x, axis=None)
+            out = reduce_amax(x.to(gpu) if x.storage_offset() == 0 else base.to(gpu)[1:], axis=None)
+            assert same_bits(out, ref), (n, x.storage_offset(), mismatch(out, ref))
+
+
+# --------------------------------------------------------------------------------------------
+# AWQ-lite search helpers: column scale and the per-alpha MSE
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_mul_cols(gpu, dtype):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(37, 4, 256, generator=g).to(dtype)
+    s = (torch.rand(256, generator=g) + 0.25).to(dtype)
+    out = ops().mul_cols(x.to(gpu), s.to(gpu))
+    assert same_bits(out, x * s), mismatch(out, x * s)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("n", [5, 4096, 12345, 1 << 22])
+def test_mse_accumulate(gpu, dtype, n):
+    """loss[i] += (a - b).float().pow(2).mean(): the difference is rounded to dtype exactly as
+    the reference does; only the summation order differs (tolerance 1e-5 relative)."""
+    g = torch.Generator().manual_seed(n)
+    a = torch.randn(n, generator=g).to(dtype)
+    b = (a.float() + 0.01 * torch.randn(n, generator=g)).to(dtype)
+    ref = (a - b).float().pow(2).double().mean()
+    loss = torch.zeros(3, device=gpu)
+    ops().mse_accumulate(a.to(gpu), b.to(gpu), loss, 1)
+    got = loss.cpu().double()
+    assert got[0] == 0 and got[2] == 0
+    torch.testing.assert_close(got[1], ref, rtol=1e-5, atol=0)
+    # deterministic: a second accumulation from the same start gives the same bits
+    loss2 = torch.zeros(3, device=gpu)
+    ops().mse_accumulate(a.to(gpu), b.to(gpu), loss2, 1)
+    assert torch.equal(loss, loss2)
