@@ -148,11 +148,12 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
 
 /* ---- AWQ-lite search helpers ---------------------------------------------------------------
  * loss[0] += mean(float(T(a - b))^2) over n elements of dtype T: the per-alpha search loss
- * `(out - out_act).float().pow(2).mean()` (model_calib.py:1555) in one read of a and b
+ * `(out - out_act).float().pow(2).mean()` (model_calib.py:1494) in one read of a and b
  * (reference: 4 ATen passes with an fp32 intermediate).  The difference is rounded to T before
  * squaring as the reference's T-typed subtraction does; the sum is fp32 per lane, double across
  * blocks, and deterministic for a given n on a given device (fixed grid, fixed final order).
- * `workspace` holds mtq_mse_workspace_floats(n, dtype) floats, zero-filled once before first
+ * `workspace` holds mtq_mse_workspace_floats(n, dtype) floats (word 0 a completion counter, then
+ * one partial per block), zero-filled once before first
  * use (the kernel leaves it reusable); one workspace per concurrently used stream. */
 int64_t mtq_mse_workspace_floats(int64_t n, int dtype);
 int mtq_mse_accumulate(const void *a, const void *b, int64_t n, int dtype, float *loss,

@@ -34,7 +34,7 @@ print(json.dumps(out))
 
 res = {}
 for rnd in range(2):
-    for v in range(4):
+    for v in range(5):
         env = dict(os.environ, MTQ_AMD_AMAX_VARIANT=str(v))
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
@@ -43,5 +43,5 @@ for rnd in range(2):
         d = json.loads(r.stdout.strip().splitlines()[-1])
         for k, val in d.items():
             res.setdefault(f"v{v}", {}).setdefault(k, []).append(val)
-print("GB/s, us per launch; v0 chunk U=8 (default), v1 grid-stride, v2 chunk U=4, v3 chunk U=16")
+print("GB/s, us per launch; v0 persistent 1024 thr U=8 2 blk/CU (default), v1 grid-stride 256 thr, v2 U=8 1 blk/CU, v3 U=8 4 blk/CU, v4 U=4 2 blk/CU")
 print(json.dumps(res, indent=1))

@@ -521,42 +521,57 @@ __global__ __launch_bounds__(kThreads) void amax_all_kernel(const T *__restrict_
   block_atomic_max(m, out);
 }
 
-// Per-tensor, chunked form (default): block b owns vectors [b*256*U, (b+1)*256*U); every lane
-// issues its U non-temporal 16 B loads before reducing any of them (U loads in flight per lane,
-// no loop-carried address math), then one atomicMax per block.  The n % N scalar tail is folded
-// into the last block.
+// Per-tensor, persistent form (default): `grid` blocks of 1024 threads (a few per CU), each
+// lane keeps U non-temporal 16 B loads in flight per round, one atomicMax per block at the end.
+// Same-address atomics serialise at ~12 ns each on gfx950 (measured: a one-vector-per-lane
+// grid of 16k blocks spends 190 us in them), so the block count, not the load pattern, is
+// what bounds a single-output reduction: keep it at O(CUs).
+constexpr int kAmaxThreads = 1024;
 template <typename T, int U>
-__global__ __launch_bounds__(kThreads) void amax_chunk_kernel(const T *__restrict__ x, int64_t n,
-                                                               int64_t nvec, uint32_t *out) {
+__global__ __launch_bounds__(kAmaxThreads) void amax_persist_kernel(const T *__restrict__ x,
+                                                                     int64_t n, int64_t nvec,
+                                                                     uint32_t *out) {
   using V = Vec<T>;
-  const int64_t base = (int64_t)blockIdx.x * kThreads * U + threadIdx.x;
+  constexpr int64_t CH = (int64_t)kAmaxThreads * U;
   uint32_t m = 0;
-  if (base + (int64_t)(U - 1) * kThreads < nvec) {
+  int64_t c0 = (int64_t)blockIdx.x * CH;
+  const int64_t step = (int64_t)gridDim.x * CH;
+  for (; c0 + CH <= nvec; c0 += step) {
     V v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ldg_vec_nt(x + (base + (int64_t)u * kThreads) * V::N);
+    for (int u = 0; u < U; ++u) v[u] = ldg_vec_nt(x + (c0 + u * kAmaxThreads + threadIdx.x) * V::N);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      uint32_t b = vec_absmax_bits(v[u]);
-      m = b > m ? b : m;
+      uint32_t bb = vec_absmax_bits(v[u]);
+      m = bb > m ? bb : m;
     }
-  } else {
+  }
+  if (c0 < nvec) {  // this block's partial chunk
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t i = base + (int64_t)u * kThreads;
+      const int64_t i = c0 + u * kAmaxThreads + threadIdx.x;
       if (i < nvec) {
-        uint32_t b = vec_absmax_bits(ldg_vec_nt(x + i * V::N));
-        m = b > m ? b : m;
+        uint32_t bb = vec_absmax_bits(ldg_vec_nt(x + i * V::N));
+        m = bb > m ? bb : m;
       }
     }
   }
   if (blockIdx.x == gridDim.x - 1) {
-    for (int64_t t = nvec * V::N + threadIdx.x; t < n; t += kThreads) {
-      uint32_t b = abs_bits_t<T>(x[t]);
-      m = b > m ? b : m;
+    for (int64_t t = nvec * V::N + threadIdx.x; t < n; t += kAmaxThreads) {
+      uint32_t bb = abs_bits_t<T>(x[t]);
+      m = bb > m ? bb : m;
     }
   }
-  block_atomic_max(m, out);
+  __shared__ uint32_t red[kAmaxThreads / 64];
+  m = wave_max_u32(m);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 1; k < kAmaxThreads / 64; ++k) m = red[k] > m ? red[k] : m;
+    atomicMax(out, m);
+  }
 }
 
 int amax_variant() {
@@ -569,10 +584,13 @@ int amax_variant() {
 }
 
 template <typename T, int U>
-int launch_amax_chunk(const T *x, int64_t n, int64_t nvec, uint32_t *out, hipStream_t stream) {
-  int64_t blocks = (nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U);
+int launch_amax_persist(const T *x, int64_t n, int64_t nvec, uint32_t *out, int per_cu,
+                        hipStream_t stream) {
+  int64_t blocks = (nvec + (int64_t)kAmaxThreads * U - 1) / ((int64_t)kAmaxThreads * U);
+  const int64_t cap = (int64_t)num_cus() * per_cu;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  amax_chunk_kernel<T, U><<<(unsigned)blocks, kThreads, 0, stream>>>(x, n, nvec, out);
+  amax_persist_kernel<T, U><<<(unsigned)blocks, kAmaxThreads, 0, stream>>>(x, n, nvec, out);
   return check_launch();
 }
 
@@ -668,11 +686,13 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
       return check_launch();
     }
     case 2:
-      return launch_amax_chunk<T, 4>(x, n, nvec, out, stream);
+      return launch_amax_persist<T, 8>(x, n, nvec, out, 1, stream);
     case 3:
-      return launch_amax_chunk<T, 16>(x, n, nvec, out, stream);
+      return launch_amax_persist<T, 8>(x, n, nvec, out, 4, stream);
+    case 4:
+      return launch_amax_persist<T, 4>(x, n, nvec, out, 2, stream);
     default:
-      return launch_amax_chunk<T, 8>(x, n, nvec, out, stream);
+      return launch_amax_persist<T, 8>(x, n, nvec, out, 2, stream);
     }
   }
   if (Q % N == 0 && al && Q >= N) {
@@ -845,24 +865,25 @@ __device__ __forceinline__ float wave_sum_f(float v) {
 }
 
 // loss[0] += sum(float(T(a - b))^2) / n -- `(out - out_act).float().pow(2).mean()`
-// (model_calib.py:1555) in one read of a and b.  Deterministic: fixed grid for a given n, each
-// block stores its partial, the last block to finish (agent-scope counter) sums the partials
-// in block order in double and resets the counter for the next call.
+// (model_calib.py:1494) in one read of a and b.  Deterministic: the grid depends only on n and
+// the CU count, each block stores its partial, and the last block to finish (agent-scope
+// counter in workspace[0]) sums the partials in block order in double, then resets the counter.
 constexpr int kMseU = 4;
+constexpr int kMseThreads = 1024;
 template <typename T>
-__global__ __launch_bounds__(kThreads) void mse_kernel(const T *__restrict__ a,
-                                                        const T *__restrict__ b, int64_t n,
-                                                        int64_t nvec, float *partials,
-                                                        unsigned *counter, float *loss) {
+__global__ __launch_bounds__(kMseThreads) void mse_kernel(const T *__restrict__ a,
+                                                           const T *__restrict__ b, int64_t n,
+                                                           int64_t nvec, unsigned *counter,
+                                                           float *partials, float *loss) {
   using V = Vec<T>;
   constexpr int N = V::N;
+  constexpr int64_t CH = (int64_t)kMseThreads * kMseU;
   float acc = 0.f;
-  const int64_t chunk = (int64_t)kThreads * kMseU;
-  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < nvec; c0 += (int64_t)gridDim.x * chunk) {
+  for (int64_t c0 = (int64_t)blockIdx.x * CH; c0 < nvec; c0 += (int64_t)gridDim.x * CH) {
     V va[kMseU], vb[kMseU];
 #pragma unroll
     for (int u = 0; u < kMseU; ++u) {
-      const int64_t i = c0 + u * kThreads + threadIdx.x;
+      const int64_t i = c0 + u * kMseThreads + threadIdx.x;
       if (i < nvec) {
         va[u] = ldg_vec_nt(a + i * N);
         vb[u] = ldg_vec_nt(b + i * N);
@@ -870,7 +891,7 @@ __global__ __launch_bounds__(kThreads) void mse_kernel(const T *__restrict__ a,
     }
 #pragma unroll
     for (int u = 0; u < kMseU; ++u) {
-      const int64_t i = c0 + u * kThreads + threadIdx.x;
+      const int64_t i = c0 + u * kMseThreads + threadIdx.x;
       if (i < nvec) {
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -881,12 +902,12 @@ __global__ __launch_bounds__(kThreads) void mse_kernel(const T *__restrict__ a,
     }
   }
   if (blockIdx.x == gridDim.x - 1) {
-    for (int64_t t = nvec * N + threadIdx.x; t < n; t += kThreads) {
+    for (int64_t t = nvec * N + threadIdx.x; t < n; t += kMseThreads) {
       float d = Elem<T>::ld(Elem<T>::st(Elem<T>::ld(a[t]) - Elem<T>::ld(b[t])));
       acc += d * d;
     }
   }
-  __shared__ float red[kThreads / 64];
+  __shared__ float red[kMseThreads / 64];
   __shared__ bool last;
   acc = wave_sum_f(acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -895,7 +916,7 @@ __global__ __launch_bounds__(kThreads) void mse_kernel(const T *__restrict__ a,
   if (threadIdx.x == 0) {
     float bs = 0.f;
 #pragma unroll
-    for (int k = 0; k < kThreads / 64; ++k) bs += red[k];
+    for (int k = 0; k < kMseThreads / 64; ++k) bs += red[k];
     __hip_atomic_store(partials + blockIdx.x, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = done == gridDim.x - 1;
@@ -913,8 +934,8 @@ __global__ __launch_bounds__(kThreads) void mse_kernel(const T *__restrict__ a,
 
 int64_t mse_grid(int64_t n, int dtype) {
   const int N = dtype == MTQ_F32 ? 4 : 8;
-  int64_t blocks = (n / N + (int64_t)kThreads * kMseU - 1) / ((int64_t)kThreads * kMseU);
-  const int64_t cap = (int64_t)num_cus() * 4;
+  int64_t blocks = (n / N + (int64_t)kMseThreads * kMseU - 1) / ((int64_t)kMseThreads * kMseU);
+  const int64_t cap = (int64_t)num_cus() * 2;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   return blocks;
@@ -1119,10 +1140,10 @@ int mtq_mse_accumulate(const void *a, const void *b, int64_t n, int dtype, float
     if (workspace_floats < grid + 1) return MTQ_ERR_INVALID_ARG;
     const bool al = aligned16(a) && aligned16(b);
     const int64_t nvec = al ? n / N : 0;
-    if (!al && n > (int64_t)kThreads * 4096) return MTQ_ERR_INVALID_ARG;  // scalar path is tail-only
-    mse_kernel<T><<<(unsigned)grid, kThreads, 0, stream>>>(
-        reinterpret_cast<const T *>(a), reinterpret_cast<const T *>(b), n, nvec, workspace,
-        reinterpret_cast<unsigned *>(workspace + grid), loss);
+    if (!al && n > (int64_t)kMseThreads * 1024) return MTQ_ERR_INVALID_ARG;  // scalar path is tail-only
+    mse_kernel<T><<<(unsigned)grid, kMseThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(a), reinterpret_cast<const T *>(b), n, nvec,
+        reinterpret_cast<unsigned *>(workspace), workspace + 1, loss);
     return check_launch();
   });
 }
