@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from .config import QuantizeConfig, algorithm_config
 from .conversion import convert_to_quantized_model, quantizer_state, set_quantizer_attributes_partial
+from .layerwise import layerwise_calibrate
 from .model_calib import awq, max_calibrate
 from .nn.modules.quant_module import QuantModule
 from .nn.modules.tensor_quantizer import SequentialQuantizer, TensorQuantizer
@@ -42,18 +43,35 @@ def _apply_algorithm(model, algo_cfg, forward_loop):
     kwargs = algo_cfg.model_dump()
     method = kwargs.pop("method")
     kwargs.pop("moe_calib_experts_ratio", None)
-    layerwise = kwargs.pop("layerwise", None)
-    if layerwise and (layerwise is True or (isinstance(layerwise, dict) and layerwise.get("enable"))):
-        raise NotImplementedError("modelopt_amd: layerwise calibration is a next-round item")
+    layerwise = kwargs.pop("layerwise", None) or {}
+    if layerwise is True:
+        layerwise = {"enable": True}
     if method == "max":
         kwargs.pop("shared_states", None)
-        max_calibrate(model, forward_loop, **kwargs)
+        func = max_calibrate
     elif method in ("awq_lite", "awq_full", "awq_clip"):
-        awq(model, forward_loop, algorithm=method, **kwargs)
+        kwargs["algorithm"] = method
+        func = awq
     elif method is None:
         return
     else:
         raise NotImplementedError(f"calibration algorithm {method!r}")
+    if layerwise.get("enable", False):
+        # reference mode.py:250-272
+        if layerwise.get("checkpoint_dir") and not layerwise.get("enable"):
+            raise ValueError("layerwise.checkpoint_dir requires layerwise.enable=True")
+        if forward_loop is None:
+            raise ValueError("forward_loop is required for calibration but got None.")
+        layerwise_calibrate(
+            model, forward_loop, func,
+            checkpoint_dir=layerwise.get("checkpoint_dir"),
+            get_qdq_activations_from_prev_layer=layerwise.get("get_qdq_activations_from_prev_layer", False),
+            save_every=layerwise.get("save_every", 1),
+            calib_mutates_weights=layerwise.get("calib_mutates_weights", True),
+            **kwargs,
+        )
+    else:
+        func(model, forward_loop, **kwargs)
 
 
 def calibrate(model: nn.Module, algorithm="max", forward_loop: Callable | None = None) -> nn.Module:

@@ -146,3 +146,29 @@ def force_eager_experts_impl_on_the_fly(model):
                 _force(getattr(cfg, sub))
 
     _force(getattr(model, "config", None))
+
+
+def _is_hf_model(model) -> bool:
+    try:
+        from transformers import PreTrainedModel
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(model, PreTrainedModel)
+
+
+def get_homogeneous_hf_decoder_layers(model):
+    """``model.model[.language_model].layers`` of an HF causal LM (reference :1799-1811)."""
+    if not _is_hf_model(model):
+        return None
+    dec = getattr(model, "model", model)
+    dec = getattr(dec, "language_model", dec)
+    return getattr(dec, "layers", None)
+
+
+def _register_layerwise_support():
+    from ..layerwise import LayerActivationCollector
+
+    LayerActivationCollector.register_decoder_layer_support(_is_hf_model, get_homogeneous_hf_decoder_layers)
+
+
+_register_layerwise_support()

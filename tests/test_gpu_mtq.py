@@ -73,6 +73,34 @@ def test_c2_tiny_llama_fp8(gpu):
     torch.testing.assert_close(logits, t["logits"], rtol=2e-3, atol=2e-3)
 
 
+def test_c2_layerwise_matches_whole_model(gpu):
+    """layerwise max calibration (qdq_from_prev False) reproduces the reference whole-model amax."""
+    import modelopt_amd.torch.quantization as mtq
+
+    t = load_file(str(G / "llama_fp8.safetensors"))
+    model = _tiny_llama()
+    model.load_state_dict({k[3:]: v for k, v in t.items() if k.startswith("sd.")})
+    model.to(gpu)
+    ids = t["calib_ids"].to(gpu)
+
+    def loop(mm):
+        for b in ids:
+            mm(b)
+
+    cfg = {**mtq.FP8_DEFAULT_CFG, "algorithm": {"method": "max", "layerwise": {"enable": True}}}
+    mtq.quantize(model, cfg, loop)
+    got = {n: q.amax for n, q in model.named_modules() if isinstance(q, mtq.TensorQuantizer) and q.amax is not None}
+    want = {k[5:]: v for k, v in t.items() if k.startswith("amax.")}
+    assert set(got) == set(want)
+    for n, v in want.items():
+        if "weight_quantizer" in n:
+            assert torch.equal(got[n].cpu(), v), n
+        else:
+            torch.testing.assert_close(got[n].cpu(), v, rtol=1e-5, atol=1e-6)
+    logits = model(t["test_ids"].to(gpu)).logits.detach().cpu()
+    torch.testing.assert_close(logits, t["logits"], rtol=2e-3, atol=2e-3)
+
+
 def _tiny_mixtral():
     from transformers import MixtralConfig, MixtralForCausalLM
 
