@@ -86,6 +86,10 @@ class _QuantModuleRegistry:
 
 QuantModuleRegistry = _QuantModuleRegistry()
 
+# data-parallel group newly converted modules sync their amax over (None = world, -1 = none);
+# layer-sharded calibration (sharded.py) switches it to -1 while it runs
+_DEFAULT_DP_GROUP = None
+
 
 class QuantModule(nn.Module):
     """Base class of quantized modules (reference :41)."""
@@ -112,7 +116,7 @@ class QuantModule(nn.Module):
         self.__dict__["_parallel_state"] = parallel_state
 
     def _initialize_parallel_state(self):
-        self.parallel_state = ParallelState(data_parallel_group=None)
+        self.parallel_state = ParallelState(data_parallel_group=_DEFAULT_DP_GROUP)
 
     def iter_weights_for_calibration(self):
         """Yield ``(weight, weight_quantizer)`` pairs for weight-only calibration."""

@@ -1,0 +1,217 @@
+"""Layer-sharded (pipelined) calibration across the GPUs of one node.
+
+The reference reaches multi-GPU calibration through Megatron / FSDP plugins and syncs each
+quantizer's amax with its own collective (tensor_quantizer.py:1373-1385).  Here the decoder layers
+of an HF causal LM are split into contiguous stages, one per rank (80 Llama-3-70B layers / 8 GPUs
+= 10 per GPU); the unchanged user ``forward_loop`` runs on every rank and the decoder-layer
+forwards are patched so that
+
+* layers before this rank's stage pass the (embedding) hidden states through untouched -- every
+  rank materialises the embedding and rotary tables so the parent forward builds real position
+  embeddings / masks, but no decoder compute happens outside the owning rank;
+* the stage's first layer replaces its input with the hidden states received from rank r-1
+  (``dist.recv`` -> RCCL point-to-point over xGMI);
+* the stage's last layer sends its output to rank r+1 and ends the forward early (the last rank
+  runs the model's tail normally).
+
+Each rank therefore calibrates exactly its own layers' quantizers on the same activations a
+single-GPU run would produce, and consecutive batches overlap across stages (batch i on stage r
+while batch i+1 is on stage r-1).  The per-stage amax state is then exchanged with ONE packed
+``all_reduce(MAX)`` over the world group (every rank ends up with the complete quantizer state,
+as export needs): owners contribute their values, other ranks zeros (amax >= 0).
+
+Decoder layers must return a tensor (transformers >= 5); models whose parent forward mixes the
+hidden state between layers are not supported (same restriction as layerwise calibration).
+"""
+
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .layerwise import LayerActivationCollector, _EarlyStopForwardError
+from .nn import SequentialQuantizer, TensorQuantizer
+from .nn.modules import quant_module as _qm
+
+__all__ = ["LayerShardPlan", "layer_shard_plan", "layer_sharded_calibration", "sync_sharded_amax"]
+
+
+@dataclass(frozen=True)
+class LayerShardPlan:
+    rank: int
+    world: int
+    first: int  # first owned decoder layer
+    last: int  # one past the last owned decoder layer
+    num_layers: int
+
+    @property
+    def owned(self) -> range:
+        return range(self.first, self.last)
+
+
+def layer_shard_plan(num_layers: int, rank: int, world: int) -> LayerShardPlan:
+    """Contiguous, balanced stages (the first ``num_layers % world`` ranks take one more)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, extra = divmod(num_layers, world)
+    first = rank * base + min(rank, extra)
+    return LayerShardPlan(rank, world, first, first + base + (1 if rank < extra else 0), num_layers)
+
+
+def _hidden_arg(args, kwargs):
+    if args:
+        return args[0], lambda h: ((h, *args[1:]), kwargs)
+    return kwargs["hidden_states"], lambda h: (args, {**kwargs, "hidden_states": h})
+
+
+@contextlib.contextmanager
+def layer_sharded_calibration(model: nn.Module, plan: LayerShardPlan, group=None):
+    """Patch ``model`` for pipelined calibration of ``plan``'s stage (see module docstring).
+
+    Inside the context every QuantModule created or converted defaults to no data-parallel amax
+    sync (the stages hold different layers; use :func:`sync_sharded_amax` afterwards).
+    """
+    layers = LayerActivationCollector.get_decoder_layers(model)
+    if layers is None:
+        raise ValueError("layer-sharded calibration needs a model with discoverable decoder layers")
+    if len(layers) != plan.num_layers:
+        raise ValueError(f"plan is for {plan.num_layers} layers, model has {len(layers)}")
+    prev_rank = plan.rank - 1 if plan.rank > 0 else None
+    next_rank = plan.rank + 1 if plan.rank + 1 < plan.world else None
+    if group is not None:
+        prev_rank = dist.get_global_rank(group, prev_rank) if prev_rank is not None else None
+        next_rank = dist.get_global_rank(group, next_rank) if next_rank is not None else None
+
+    saved = []
+
+    def patch(m, fn):
+        saved.append((m, m.__dict__.get("forward")))
+        orig = m.forward
+        m.forward = fn(orig).__get__(m)
+
+    def passthrough(orig):
+        def f(mod, *args, **kwargs):
+            h, _ = _hidden_arg(args, kwargs)
+            return h
+
+        return f
+
+    def stage_layer(orig, i):
+        def f(mod, *args, **kwargs):
+            if i == plan.first and prev_rank is not None:
+                h, rebuild = _hidden_arg(args, kwargs)
+                buf = torch.empty(h.shape, dtype=h.dtype, device=_device_of(mod, h))
+                dist.recv(buf, src=prev_rank, group=group)
+                args, kwargs = rebuild(buf)
+            out = orig(*args, **kwargs)
+            if i == plan.last - 1 and next_rank is not None:
+                if not isinstance(out, torch.Tensor):
+                    raise TypeError("layer-sharded calibration needs decoder layers that return a tensor")
+                dist.send(out.contiguous(), dst=next_rank, group=group)
+                raise _EarlyStopForwardError()
+            return out
+
+        return f
+
+    def model_fwd(orig):
+        def f(mod, *args, **kwargs):
+            try:
+                return orig(*args, **kwargs)
+            except _EarlyStopForwardError:
+                return None
+
+        return f
+
+    prev_default = _qm._DEFAULT_DP_GROUP
+    _qm._DEFAULT_DP_GROUP = -1
+    try:
+        for i, layer in enumerate(layers):
+            if i < plan.first:
+                patch(layer, passthrough)
+            elif i < plan.last:
+                patch(layer, lambda o, i=i: stage_layer(o, i))
+            # layers past the stage are never reached (early stop), except on the last rank
+        patch(model, model_fwd)
+        for m in model.modules():
+            if isinstance(m, _qm.QuantModule):
+                m.parallel_state = _qm.ParallelState(data_parallel_group=-1)
+        yield plan
+    finally:
+        _qm._DEFAULT_DP_GROUP = prev_default
+        for m, fwd in reversed(saved):
+            m.__dict__.pop("forward", None)
+            if fwd is not None:
+                m.__dict__["forward"] = fwd
+
+
+def _device_of(mod: nn.Module, like: torch.Tensor) -> torch.device:
+    for p in mod.parameters():
+        if p.device.type != "meta":
+            return p.device
+    return like.device
+
+
+def _leaf_quantizers(model: nn.Module):
+    for name, m in model.named_modules():
+        if isinstance(m, TensorQuantizer) and not isinstance(m, SequentialQuantizer):
+            yield name, m
+
+
+@torch.no_grad()
+def sync_sharded_amax(model: nn.Module, device=None, group=None) -> int:
+    """Give every rank the complete amax state after layer-sharded calibration.
+
+    Shapes of the owned (real) amax buffers are exchanged as small host objects; the values
+    travel in ONE packed fp32 ``all_reduce(MAX)`` on ``device`` (RCCL on MI355X).  Returns the
+    number of amax entries in the packed buffer.
+    """
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0
+    mine = {}
+    for name, q in _leaf_quantizers(model):
+        a = getattr(q, "_amax", None)
+        if isinstance(a, torch.Tensor) and a.device.type != "meta":
+            mine[name] = (tuple(a.shape), str(a.dtype).replace("torch.", ""))
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine, group=group)
+    layout = {}
+    for d in gathered:
+        for k, v in d.items():
+            if k in layout and layout[k] != v:
+                raise RuntimeError(f"amax shape/dtype of {k} differs across ranks: {layout[k]} vs {v}")
+            layout[k] = v
+    names = sorted(layout)
+    sizes = [int(torch.Size(layout[n][0]).numel()) for n in names]
+    total = sum(sizes)
+    if device is None:
+        device = next((getattr(q, "_amax").device for n, q in _leaf_quantizers(model) if n in mine), None)
+        device = device or torch.device("cuda", torch.cuda.current_device())
+    flat = torch.zeros(total, dtype=torch.float32, device=device)
+    mods = dict(_leaf_quantizers(model))
+    off = 0
+    for n, k in zip(names, sizes):
+        if n in mine:
+            flat[off : off + k] = mods[n]._amax.detach().reshape(-1).to(device=device, dtype=torch.float32)
+        off += k
+    if dist.get_backend(group) == "gloo" and flat.device.type != "cpu":
+        c = flat.cpu()
+        dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+        flat = c.to(device)
+    else:
+        dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=group)
+    off = 0
+    for n, k in zip(names, sizes):
+        shape, dt = layout[n]
+        val = flat[off : off + k].view(shape).to(getattr(torch, dt))
+        q = mods.get(n)
+        if q is not None:
+            if n not in mine and hasattr(q, "_amax"):
+                delattr(q, "_amax")  # a meta placeholder from weight-only calibration
+            q.amax = val
+        off += k
+    return total
