@@ -15,6 +15,7 @@ point-to-point; the stages' amax state is exchanged with one packed all_reduce(M
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -84,7 +85,8 @@ def build_sharded(layers: int, device, plan=None):
     return model.eval()
 
 
-def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", mode="pipeline"):
+def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", mode="pipeline",
+        algorithm="max", eval_batches=4):
     import modelopt_amd.torch.quantization as mtq
     from modelopt_amd.torch.quantization.sharded import (
         layer_shard_plan,
@@ -116,28 +118,49 @@ def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", m
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if mode == "pipeline":
-        with layer_sharded_calibration(model, plan):
-            mtq.quantize(model, getattr(mtq, config), forward_loop)
-        n_amax = sync_sharded_amax(model, device=dev)
-    else:
-        mtq.quantize(model, getattr(mtq, config), forward_loop)
-        n_amax = None
+    # MX presets are dynamic (algorithm None); "max" collects the per-tensor amax anyway so the
+    # exported state carries it -- that is the amax the stages exchange
+    cfg = {**getattr(mtq, config), "algorithm": None if algorithm == "none" else algorithm}
+    def ctx():
+        return layer_sharded_calibration(model, plan) if mode == "pipeline" else contextlib.nullcontext()
+
+    with ctx():
+        mtq.quantize(model, cfg, forward_loop)
+    n_amax = sync_sharded_amax(model, device=dev) if mode == "pipeline" else None
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if dist.is_initialized():
-        t = torch.tensor([wall], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = _max_over_ranks(time.perf_counter() - t0, dev)
+
+    # the fake-quant hot path at scale: MXFP4 W+A quantized forward over `eval_batches` batches
+    ev = batches[:eval_batches]
+    with ctx(), torch.no_grad():
+        model(ev[0])  # warm-up
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        t0 = time.perf_counter()
+        for b in ev:
+            model(b)
+        torch.cuda.synchronize()
+    qfwd = _max_over_ranks(time.perf_counter() - t0, dev)
     res = {
         "model": f"Llama-3-70B dims, {layers} layers, bf16 random init", "config": config, "mode": mode,
         "world": world, "samples": samples, "seq": seq, "batch": batch,
         "stage_layers": None if plan is None else [plan.first, plan.last],
+        "algorithm": algorithm,
         "ptq_wall_clock_s": round(wall, 3), "calib_tokens_per_s": round(samples * seq / wall, 1),
+        "qdq_forward_tokens_per_s": round(len(ev) * batch * seq * (1 if mode == "pipeline" else world) / qfwd, 1),
         "build_s": round(build_s, 1), "packed_amax_entries": n_amax,
         "hbm_gb_rank0": round(torch.cuda.max_memory_allocated() / 1e9, 1),
     }
     return res
+
+
+def _max_over_ranks(v: float, dev) -> float:
+    if dist.is_initialized():
+        t = torch.tensor([v], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        v = float(t.item())
+    return v
 
 
 def main():
@@ -148,6 +171,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--config", default="MXFP4_DEFAULT_CFG")
     ap.add_argument("--mode", choices=["pipeline", "dp"], default="pipeline")
+    ap.add_argument("--algorithm", default="max", help='"max" or "none" (the MX preset as is)')
+    ap.add_argument("--eval-batches", type=int, default=4)
     a = ap.parse_args()
     if "RANK" in os.environ:
         local = int(os.environ.get("LOCAL_RANK", 0))
@@ -155,7 +180,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    res = run(a.samples, a.seq, a.batch, a.layers, a.config, a.mode)
+    res = run(a.samples, a.seq, a.batch, a.layers, a.config, a.mode, a.algorithm, a.eval_batches)
     if not dist.is_initialized() or dist.get_rank() == 0:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():

@@ -120,7 +120,7 @@ class LayerActivationCollector:
             if st.mode == "run":
                 assert st.cached_inputs, f"layer {st.name} has no cached inputs to replay"
                 a, k = st.cached_inputs.popleft()
-                out = mod.__dict__["_lw_original_forward"](*a, **k)
+                out = mod.__dict__["_lw_original_forward"](*a, **_fresh_kwargs(k))
                 st.output_meta = _output_meta(out)
                 return out
             if st.mode == "capture":
@@ -308,19 +308,18 @@ def _map_tensors(obj, fn):
     return obj
 
 
+def _fresh_kwargs(k: dict) -> dict:
+    """A replayed layer must start from an empty KV cache: drop the captured cache object (its
+    contents depend on which replays already ran; transformers-5 ``DynamicCache.reset`` zeroes
+    but keeps the cached length, which would corrupt the attention)."""
+    if k.get("past_key_values") is not None:
+        k = dict(k)
+        k["past_key_values"] = None
+    return k
+
+
 def _strip_cache(inputs: list) -> list:
-    """Drop KV caches from captured kwargs: a replayed layer must start from an empty cache."""
-    out = []
-    for a, k in inputs:
-        if k.get("past_key_values") is not None:
-            k = dict(k)
-            cache = k["past_key_values"]
-            if hasattr(cache, "reset"):
-                cache.reset()
-            else:
-                k["past_key_values"] = None
-        out.append((a, k))
-    return out
+    return [(a, _fresh_kwargs(k)) for a, k in inputs]
 
 
 @torch.no_grad()

@@ -17,10 +17,13 @@ def _tiny_llama(layers=4):
     return LlamaForCausalLM(cfg).eval()
 
 
-def _reference_inputs(model, batches):
+def _reference_inputs(model, batches, sub=None):
+    """Inputs each decoder layer (or its submodule ``sub``, e.g. the attention output projection)
+    receives in a whole-model forward."""
     seen = {i: [] for i in range(len(model.model.layers))}
-    hooks = [layer.register_forward_pre_hook(lambda m, a, k, i=i: seen[i].append(a[0].clone() if a else k["hidden_states"].clone()), with_kwargs=True)
-             for i, layer in enumerate(model.model.layers)]
+    mods = [layer.get_submodule(sub) if sub else layer for layer in model.model.layers]
+    hooks = [m.register_forward_pre_hook(lambda m, a, k, i=i: seen[i].append(a[0].clone() if a else k["hidden_states"].clone()), with_kwargs=True)
+             for i, m in enumerate(mods)]
     with torch.no_grad():
         for b in batches:
             model(b)
@@ -41,20 +44,26 @@ def test_layerwise_inputs_match_whole_model(use_cache):
     g = torch.Generator().manual_seed(1)
     batches = [torch.randint(0, 50, (2, 12), generator=g) for _ in range(3)]
     want = _reference_inputs(m, batches)
-    got = {}
+    want_o = _reference_inputs(m, batches, "self_attn.o_proj")
+    got, got_o = {}, {}
 
     def calib(layer, loop):
         idx = list(m.model.layers).index(layer)
-        got[idx] = []
+        got[idx], got_o[idx] = [], []
         h = layer.register_forward_pre_hook(lambda mod, a, k: got[idx].append(a[0].clone() if a else k["hidden_states"].clone()), with_kwargs=True)
+        h2 = layer.self_attn.o_proj.register_forward_pre_hook(lambda mod, a: got_o[idx].append(a[0].clone()))
         loop(layer)
+        loop(layer)  # a second replay (e.g. AWQ's cache + search passes) must see the same thing
         h.remove()
+        h2.remove()
 
     layerwise_calibrate(m, lambda mm: [mm(b) for b in batches], calib)
     assert sorted(got) == list(range(4))
     for i in range(4):
-        assert len(got[i]) == 3
-        for a, b in zip(got[i], want[i]):
+        assert len(got[i]) == 6 and len(got_o[i]) == 6
+        for a, b in zip(got[i], want[i] + want[i]):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+        for a, b in zip(got_o[i], want_o[i] + want_o[i]):  # attention saw an empty KV cache
             torch.testing.assert_close(a, b, rtol=0, atol=0)
     # unpatched afterwards: the model runs normally
     assert "forward" not in m.__dict__ and all("forward" not in l.__dict__ for l in m.model.layers)
