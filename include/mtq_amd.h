@@ -146,6 +146,17 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
 int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                       int skip_zeros, uint32_t *counts, hipStream_t stream);
 
+/* ---- NVFP4 --------------------------------------------------------------------------------
+ * Two-level dynamic NVFP4 fake quant of x [rows, cols] (blocks of block_size along cols, zero
+ * padded): the reference's primary NVFP4 kernel, fp4_fake_quant_block
+ * (kernels/quantization/gemm/fp4_kernel_hopper.py:102-160, dispatched from
+ * tensor_quant.py:173-181 for num_bits (2,1) / scale_bits (4,3)).  global_amax is a device fp32
+ * scalar; per block the FP8-E4M3-quantised scale q = e4m3(min(bmax / (6 gs), 448)) * gs with
+ * gs = global_amax / 2688, then y = sign(x) * e2m1(|x| / q) * q.  block_size in {8, 16, 32}
+ * (the reference always passes its default, 16). */
+int mtq_nvfp4_fake_quant(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
+                         const float *global_amax, int block_size, hipStream_t stream);
+
 /* ---- AWQ-lite search helpers ---------------------------------------------------------------
  * loss[0] += mean(float(T(a - b))^2) over n elements of dtype T: the per-alpha search loss
  * `(out - out_act).float().pow(2).mean()` (model_calib.py:1494) in one read of a and b

@@ -338,9 +338,37 @@ def e8m0_scale(amax, fmt):
     return torch.where(bad, one, scale), torch.where(bad, one, unscale)
 
 
-def fused_amax_convert(x, block_size, fmt, scale_fmt="E8M0"):
-    """Per-block (last dim) dynamic quant, zero-padded partial blocks (tensor_quant_mx.cu:316-352)."""
-    assert scale_fmt == "E8M0", "oracle covers the E8M0 (MX) scale format"
+def _generic_scale(amax, fmt, scale_fmt):
+    """compute_scale's general path (tensor_quant_mx.cu:147-153): fp32 emax/amax widened to
+    double, 1/scale rounded to fp32 and converted to the scale format, scale = 1/inv in double."""
+    emax = FORMAT_MAX[fmt]
+    sc = (torch.tensor(emax, dtype=torch.float32) / amax.float()).double()
+    inv = convert_to_types((1.0 / sc).float(), scale_fmt).double()
+    scale, unscale = (1.0 / inv).float(), inv.float()
+    bad = (amax == 0) | torch.isinf(amax) | torch.isnan(amax)
+    one = torch.ones_like(scale)
+    return torch.where(bad, one, scale), torch.where(bad, one, unscale)
+
+
+def _global_scale(gamax, lamax, fmt, scale_fmt):
+    """compute_scale_with_global (tensor_quant_mx.cu:156-183)."""
+    em = torch.tensor(FORMAT_MAX[fmt], dtype=torch.float32)
+    sm = FORMAT_MAX[scale_fmt]
+    gamax = gamax.float()
+    local_unscale = lamax.float() / em  # fp32
+    two_level = sm * (em / gamax).double()  # double(fp32 ratio) * double(scale max)
+    luq = convert_to_types((local_unscale.double() * two_level).float(), scale_fmt).double() / two_level
+    scale, unscale = (1.0 / luq).float(), luq.float()
+    bad = (lamax == 0) | torch.isinf(lamax) | torch.isnan(lamax) | (gamax == 0) | torch.isinf(gamax) | torch.isnan(gamax)
+    one = torch.ones_like(scale)
+    return torch.where(bad, one, scale), torch.where(bad, one, unscale)
+
+
+def fused_amax_convert(x, block_size, fmt, scale_fmt="E8M0", global_amax=None):
+    """Per-block (last dim) dynamic quant, zero-padded partial blocks (tensor_quant_mx.cu:240-387),
+    E8M0 / generic / two-level (global amax) scales.  Per-channel global amax when x is 2-D and
+    global_amax has x.size(0) elements (get_global_scaling :296-310; the reference indexes it with
+    the padded element index / actual cols, i.e. the row whenever cols % block_size == 0)."""
     if block_size not in (8, 16, 32):
         raise ValueError("Blocksize for fused call must be one of {8, 16, 32}")
     dtype = x.dtype
@@ -352,10 +380,45 @@ def fused_amax_convert(x, block_size, fmt, scale_fmt="E8M0"):
     blocks = xp.reshape(xp.shape[0], -1, block_size)
     amax = blocks.abs().clamp(max=torch.finfo(torch.float32).max)
     amax = torch.where(torch.isnan(amax), torch.zeros_like(amax), amax).amax(-1, keepdim=True)
-    scale, unscale = e8m0_scale(amax, fmt)
+    if global_amax is not None:
+        g = global_amax.float().reshape(-1)
+        if x.dim() == 2 and g.numel() == x.shape[0]:
+            ga = g.view(-1, 1, 1).expand_as(amax)
+        else:
+            ga = g[0].expand_as(amax)
+        scale, unscale = _global_scale(ga, amax, fmt, scale_fmt)
+    elif scale_fmt == "E8M0":
+        scale, unscale = e8m0_scale(amax, fmt)
+    else:
+        scale, unscale = _generic_scale(amax, fmt, scale_fmt)
     a = blocks.abs() * scale
     q = convert_to_types(a, fmt) * unscale
     y = torch.where(blocks < 0, -q, q)
+    y = y.reshape(xp.shape)[:, :cols]
+    return y.reshape(shape).to(dtype)
+
+
+def nvfp4_fake_quant_block(x, global_amax, block_size=16):
+    """NVFP4 dynamic two-level fake quant as the reference's primary kernel computes it
+    (kernels/quantization/gemm/fp4_kernel_hopper.py:33-160 with common/nvfp4_quant.py
+    fp8_quantize_scale / fp4_round_magnitude), in fp32 with correctly rounded divisions."""
+    dtype, shape = x.dtype, x.shape
+    xf = x.float().reshape(-1, shape[-1])
+    cols = shape[-1]
+    pad = (-cols) % block_size
+    xp = torch.nn.functional.pad(xf, (0, pad)) if pad else xf
+    blocks = xp.reshape(xp.shape[0], -1, block_size)
+    gs = global_amax.float().reshape(()) / torch.tensor(6.0 * 448.0, dtype=torch.float32)
+    gs = torch.where(gs > 0, gs, torch.tensor(1e-12, dtype=torch.float32))
+    bmax = blocks.abs().amax(-1, keepdim=True)
+    s8 = bmax / (torch.tensor(6.0, dtype=torch.float32) * gs)
+    s8 = torch.minimum(s8, torch.tensor(448.0))
+    q8 = s8.to(torch.float8_e4m3fn).float() * gs
+    q8 = torch.where(q8 >= 1e-5, q8, torch.ones_like(q8))
+    a = blocks.abs() / q8
+    q = _table_round(a, "E2M1")
+    r = q * q8
+    y = torch.where(blocks >= 0, r, -r)
     y = y.reshape(xp.shape)[:, :cols]
     return y.reshape(shape).to(dtype)
 

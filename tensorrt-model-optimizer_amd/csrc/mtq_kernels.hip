@@ -393,8 +393,10 @@ __device__ __forceinline__ float mx_qdq(float x, float scale, float unscale, int
 
 // Fast path: cols % bs == 0 and 16-byte aligned rows, so blocks never straddle rows and the
 // tensor is a flat sequence of blocks.  LPB = lanes per block = bs / N (N elements per lane);
-// the block amax is a shuffle-max over LPB adjacent lanes (<= 8 lanes: one DPP row).
-template <typename T, int BS>
+// the block amax is a shuffle-max over LPB adjacent lanes (<= 8 lanes: one DPP row).  FMT >= 0
+// bakes the element format in at compile time (the per-element conversion is the kernel's only
+// real ALU work: with a runtime format it was VALU-bound at ~4.3 TB/s); FMT = -1 reads p.fmt.
+template <typename T, int BS, int FMT>
 __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ x,
                                                            T *__restrict__ y, int64_t nvec,
                                                            MxParams p) {
@@ -402,6 +404,7 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   constexpr int N = V::N;
   constexpr int LPB = BS / N >= 1 ? BS / N : 1;
   static_assert(BS % N == 0, "block must be a multiple of the vector");
+  const int fmt = FMT >= 0 ? FMT : p.fmt;
   // nvec % LPB == 0 and kThreads % LPB == 0: the LPB lanes of an MX block are all live or all out
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i - (threadIdx.x % LPB) >= nvec) return;
@@ -411,13 +414,31 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   for (int j = 0; j < N; ++j) m = fmaxf(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
   m = group_max_f<LPB>(m);
   const int64_t blk = i / LPB;
-  const int64_t row = (blk * BS) / p.cols;
   float scale, unscale;
-  mx_block_scale(m, row, p, scale, unscale);
+  if (p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
+    e8m0_scale(m, format_max(fmt), scale, unscale);
+  } else {
+    const int64_t row = (blk * BS) / p.cols;
+    mx_block_scale(m, row, p, scale, unscale);
+  }
 #pragma unroll
   for (int j = 0; j < N; ++j)
-    v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, p.fmt));
+    v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, fmt));
   stg_vec_nt(y + i * N, v);
+}
+
+template <typename T, int BS>
+void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t stream) {
+  const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
+  switch (p.fmt) {
+  case MTQ_E2M1: mx_vec_kernel<T, BS, MTQ_E2M1><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  case MTQ_E4M3: mx_vec_kernel<T, BS, MTQ_E4M3><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  case MTQ_E5M2: mx_vec_kernel<T, BS, MTQ_E5M2><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  case MTQ_INT8: mx_vec_kernel<T, BS, MTQ_INT8><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  case MTQ_E3M2: mx_vec_kernel<T, BS, MTQ_E3M2><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  case MTQ_E2M3: mx_vec_kernel<T, BS, MTQ_E2M3><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  default: mx_vec_kernel<T, BS, -1><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  }
 }
 
 // General path: one lane per element of the zero-padded [rows, padded_cols] matrix; BS lanes
@@ -454,11 +475,10 @@ int launch_mx(const void *xv, void *yv, int64_t rows, int64_t cols, int bs, MxPa
   const int64_t n = rows * cols;
   if (cols % bs == 0 && bs % N == 0 && aligned16(x) && aligned16(y)) {
     int64_t nvec = n / N;
-    unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
     switch (bs) {
-    case 8: mx_vec_kernel<T, 8><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-    case 16: mx_vec_kernel<T, 16><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-    case 32: mx_vec_kernel<T, 32><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+    case 8: launch_mx_vec<T, 8>(x, y, nvec, p, stream); break;
+    case 16: launch_mx_vec<T, 16>(x, y, nvec, p, stream); break;
+    case 32: launch_mx_vec<T, 32>(x, y, nvec, p, stream); break;
     default: return MTQ_ERR_BLOCKSIZE;
     }
     return check_launch();
@@ -941,6 +961,102 @@ int64_t mse_grid(int64_t n, int dtype) {
   return blocks;
 }
 
+
+// ============================================================================================
+// NVFP4 two-level dynamic block fake quant (the reference's primary NVFP4 kernel,
+// kernels/quantization/gemm/fp4_kernel_hopper.py:33-160 + common/nvfp4_quant.py)
+// ============================================================================================
+// gs = RN(global_amax / 2688) (1e-12 when not > 0); per block of BS along the last dim:
+// s8 = min(RN(bmax / RN(6 gs)), 448); q = fp32(e4m3_rne(s8)) * gs (1 when < 1e-5);
+// y = sign(x) * e2m1(RN(|x| / q)) * q, E2M1 = round-to-nearest-even on {0,.5,1,1.5,2,3,4,6},
+// saturating (NaN -> 6 like the reference's comparison chain).  Divisions are correctly rounded
+// (Markstein on RN(1/q)), as the reference's fp32 `/` is.
+struct Nvfp4Block {
+  float q, r;  // block scale and RN(1/q)
+};
+
+__device__ __forceinline__ Nvfp4Block nvfp4_block(float bmax, float gs) {
+  const float six_gs = 6.0f * gs;
+  float s8 = div_rn(bmax, six_gs, 1.0f / six_gs);
+  s8 = s8 < 448.0f ? s8 : 448.0f;  // NaN -> 448 (tl.minimum returns the non-NaN operand)
+  const int p = __builtin_amdgcn_cvt_pk_fp8_f32(s8, s8, 0, false);
+  float q = __builtin_amdgcn_cvt_f32_fp8(p, 0) * gs;
+  q = q >= 1e-5f ? q : 1.0f;
+  return {q, 1.0f / q};
+}
+
+__device__ __forceinline__ float nvfp4_qdq(float x, const Nvfp4Block &b) {
+  const float a = div_rn(fabsf(x), b.q, b.r);
+  const float c = round_table(a, TableFmt{1, 0, 6.0f, false}) * b.q;
+  return x >= 0.f ? c : -c;
+}
+
+__device__ __forceinline__ float nvfp4_global_scale(const float *gamax) {
+  const float g = *gamax;
+  const float gs = div_rn(g, 2688.0f, 1.0f / 2688.0f);
+  return gs > 0.f ? gs : 1e-12f;
+}
+
+template <typename T, int BS>
+__global__ __launch_bounds__(kThreads) void nvfp4_vec_kernel(const T *__restrict__ x,
+                                                              T *__restrict__ y, int64_t nvec,
+                                                              const float *__restrict__ gamax) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  constexpr int LPB = BS / N;
+  static_assert(BS % N == 0, "block must be a multiple of the vector");
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i - (threadIdx.x % LPB) >= nvec) return;
+  const float gs = nvfp4_global_scale(gamax);
+  V v = ldg_vec_nt(x + i * N);
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) m = fmaxf(m, fabsf(Elem<T>::ld(v.e[j])));
+  m = group_max_f<LPB>(m);
+  const Nvfp4Block b = nvfp4_block(m, gs);
+#pragma unroll
+  for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(nvfp4_qdq(Elem<T>::ld(v.e[j]), b));
+  stg_vec_nt(y + i * N, v);
+}
+
+// any shape: one lane per element of the zero-padded [rows, pcols] matrix, BS lanes per block
+template <typename T, int BS>
+__global__ __launch_bounds__(kThreads) void nvfp4_scalar_kernel(const T *__restrict__ x,
+                                                                 T *__restrict__ y, int64_t rows,
+                                                                 int64_t cols, int64_t pcols,
+                                                                 const float *__restrict__ gamax) {
+  const float gs = nvfp4_global_scale(gamax);
+  const int64_t total = rows * pcols;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx - (threadIdx.x % BS) < total;
+       idx += stride) {
+    const bool live = idx < total;
+    const int64_t row = live ? idx / pcols : 0;
+    const int64_t col = live ? idx - row * pcols : 0;
+    const bool real = live && col < cols;
+    const float v = real ? Elem<T>::ld(x[row * cols + col]) : 0.f;
+    const float m = group_max_f<BS>(fabsf(v));
+    if (!real) continue;
+    y[row * cols + col] = Elem<T>::st(nvfp4_qdq(v, nvfp4_block(m, gs)));
+  }
+}
+
+template <typename T, int BS>
+int launch_nvfp4(const T *x, T *y, int64_t rows, int64_t cols, const float *gamax,
+                 hipStream_t stream) {
+  constexpr int N = Vec<T>::N;
+  if (cols % BS == 0 && BS % N == 0 && aligned16(x) && aligned16(y)) {
+    const int64_t nvec = rows * cols / N;
+    nvfp4_vec_kernel<T, BS><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+        x, y, nvec, gamax);
+  } else {
+    const int64_t pcols = (cols + BS - 1) / BS * BS;
+    nvfp4_scalar_kernel<T, BS><<<grid_for(rows * pcols, kThreads), kThreads, 0, stream>>>(
+        x, y, rows, cols, pcols, gamax);
+  }
+  return check_launch();
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1163,6 +1279,24 @@ int mtq_mul_cols(const void *x, const void *scale, void *y, int64_t rows, int64_
         reinterpret_cast<const T *>(x), reinterpret_cast<const T *>(scale),
         reinterpret_cast<T *>(y), nvec, cols);
     return check_launch();
+  });
+}
+
+int mtq_nvfp4_fake_quant(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
+                         const float *global_amax, int block_size, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || !global_amax || (rows * cols > 0 && (!x || !y)))
+    return MTQ_ERR_INVALID_ARG;
+  if (block_size != 8 && block_size != 16 && block_size != 32) return MTQ_ERR_BLOCKSIZE;
+  if (rows * cols == 0) return MTQ_OK;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    const T *xt = reinterpret_cast<const T *>(x);
+    T *yt = reinterpret_cast<T *>(y);
+    switch (block_size) {
+    case 8: return launch_nvfp4<T, 8>(xt, yt, rows, cols, global_amax, stream);
+    case 16: return launch_nvfp4<T, 16>(xt, yt, rows, cols, global_amax, stream);
+    default: return launch_nvfp4<T, 32>(xt, yt, rows, cols, global_amax, stream);
+    }
   });
 }
 

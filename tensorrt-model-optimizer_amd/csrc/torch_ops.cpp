@@ -13,6 +13,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -341,6 +342,24 @@ at::Tensor mul_cols(const at::Tensor &x, const at::Tensor &scale) {
   return y;
 }
 
+at::Tensor nvfp4_fake_quant_block(const at::Tensor &inputs, const at::Tensor &global_amax,
+                                  int64_t block_size) {
+  check_device(inputs, "inputs");
+  const int dt = checked_dtype(inputs, "inputs");
+  TORCH_CHECK(dt != MTQ_F64, "nvfp4_fake_quant_block: float64 is not supported");
+  at::Tensor x = inputs.contiguous();
+  at::Tensor y = at::empty_like(x);
+  if (x.numel() == 0) return y;
+  at::Tensor g = global_amax.to(x.device(), at::kFloat).contiguous();
+  TORCH_CHECK(g.numel() == 1, "nvfp4_fake_quant_block: global_amax must be a scalar");
+  const int64_t cols = x.dim() == 0 ? 1 : x.size(-1);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_nvfp4_fake_quant(x.data_ptr(), y.data_ptr(), x.numel() / cols, cols, dt,
+                                g.data_ptr<float>(), (int)block_size, cur_stream(x));
+  check_status(st, "nvfp4_fake_quant_block");
+  return y;
+}
+
 at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at::Tensor> &pqs,
                                int64_t block, int64_t num_bits, bool is_unsigned,
                                bool narrow_range) {
@@ -403,6 +422,9 @@ int format_code(int64_t e, int64_t m, bool is_int) {
   return -1;
 }
 
+// mirrors tensor_quant.DISABLE_TRITON_KERNEL (tensor_quant.py:43)
+std::atomic<bool> g_disable_nvfp4_kernel{false};
+
 at::Tensor dynamic_block_quantize_op(const at::Tensor &input, int64_t block_size,
                                      const c10::optional<at::Tensor> &amax, int64_t num_bits,
                                      int64_t exponent_bits, int64_t scale_num_bits,
@@ -424,8 +446,14 @@ at::Tensor dynamic_block_quantize_op(const at::Tensor &input, int64_t block_size
                 "amax must be a CUDA tensor for dynamic block quantization.");
     g = amax->numel() != 1 ? amax->amax() : *amax;
   }
+  // NVFP4 goes to the reference's primary kernel (fp4_fake_quant_block, default block 16,
+  // tensor_quant.py:173-181) unless DISABLE_TRITON_KERNEL routes it to fused_amax_convert
+  if (fmt == MTQ_E2M1 && sfmt == MTQ_E4M3 && !g_disable_nvfp4_kernel.load())
+    return nvfp4_fake_quant_block(input, *g, 16);
   return fused_amax_convert(input, block_size, fmt, sfmt, g);
 }
+
+void set_disable_triton_kernel(bool v) { g_disable_nvfp4_kernel.store(v); }
 
 at::Tensor meta_like(const at::Tensor &x) { return at::empty_like(x); }
 
@@ -454,6 +482,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "bool skip_zeros) -> ()");
   m.def("mse_accumulate(Tensor a, Tensor b, Tensor(a!) loss, int index) -> ()");
   m.def("mul_cols(Tensor inputs, Tensor scale) -> Tensor");
+  m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
+  m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
@@ -471,6 +501,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);
   m.impl("mse_accumulate", &mse_accumulate);
   m.impl("mul_cols", &mul_cols);
+  m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
@@ -499,5 +530,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
            return meta_like(x);
          });
   m.impl("mul_cols", [](const at::Tensor &x, const at::Tensor &) { return meta_like(x); });
+  m.impl("nvfp4_fake_quant_block",
+         [](const at::Tensor &x, const at::Tensor &, int64_t) { return meta_like(x); });
   m.impl("mse_accumulate", [](const at::Tensor &, const at::Tensor &, at::Tensor, int64_t) {});
 }

@@ -54,11 +54,21 @@ def quantize_op(input, amax, num_bits=8, exponent_bits=0, unsigned=False, narrow
     return _ops().quantize_op(input, amax, num_bits, exponent_bits, unsigned, narrow_range)
 
 
+# tensor_quant.py:43 -- True routes NVFP4 (E2M1 + E4M3 scales) to fused_amax_convert instead of
+# the fp4_fake_quant_block kernel (the reference's Triton kernel; here the HIP nvfp4 kernel)
+DISABLE_TRITON_KERNEL = False
+_disable_synced = [None]
+
+
 def dynamic_block_quantize_op(
     input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
 ):
     """``tensorrt::dynamic_block_quantize_op`` schema (tensor_quant.py:227-231)."""
-    return _ops().dynamic_block_quantize_op(
+    ops = _ops()
+    if _disable_synced[0] is not DISABLE_TRITON_KERNEL:
+        ops.set_disable_triton_kernel(bool(DISABLE_TRITON_KERNEL))
+        _disable_synced[0] = DISABLE_TRITON_KERNEL
+    return ops.dynamic_block_quantize_op(
         input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
     )
 

@@ -57,6 +57,10 @@ def _make_shim():
 
 _make_shim()
 
+# the reference's Triton kernels (NVFP4 golden) run on CPU through the Triton interpreter; it
+# must be selected before any @triton.jit decoration happens
+os.environ.setdefault("TRITON_INTERPRET", "1")
+
 import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
 from safetensors.torch import save_file as _save_file  # noqa: E402
@@ -352,6 +356,71 @@ def gen_awq():
     (OUT / "awq.json").write_text(json.dumps(meta, indent=1))
 
 
+def gen_nvfp4():
+    """NVFP4 dynamic two-level fake quant from the reference's own Triton kernel
+    (kernels/quantization/gemm/fp4_kernel_hopper.py fp4_fake_quant_block), run on CPU with the
+    Triton interpreter (TRITON_INTERPRET=1; its cuda-device context is bypassed for CPU tensors).
+
+    The Triton 3.6 interpreter's casts are not all the hardware's.  Its fp32 -> bf16 store
+    truncates (handled by running the kernel in fp32 and rounding with torch, see below).  Its
+    fp32 -> float8e4nv cast it truncates where
+    round-to-nearest carries into the next binade (1.97 -> 1.0, not 2.0) and flushes small values
+    to 0 (checked below against torch's RNE cast, which is what cvt.rn.satfinite computes).  The
+    per-block scale goes through that cast, so the blocks whose scale hits such a value are
+    recorded in ``mask`` and excluded from the comparison; everything else is pinned."""
+    import contextlib
+    import importlib
+
+    import triton
+    import triton.language as tl
+
+    torch.cuda.device = lambda d: contextlib.nullcontext()  # the wrapper's context, CPU tensors
+    hop = importlib.import_module("modelopt.torch.kernels.quantization.gemm.fp4_kernel_hopper")
+
+    @triton.jit
+    def _cast_fp8(x_ptr, y_ptr, n, BLOCK: tl.constexpr):
+        o = tl.arange(0, BLOCK)
+        x = tl.load(x_ptr + o, mask=o < n, other=0.0)
+        tl.store(y_ptr + o, x.to(tl.float8e4nv).to(tl.float32), mask=o < n)
+
+    def interp_cast_ok(s8):
+        flat = s8.reshape(-1).contiguous()
+        out = torch.empty_like(flat)
+        blk = triton.next_power_of_2(max(flat.numel(), 1))
+        _cast_fp8[(1,)](flat, out, flat.numel(), BLOCK=blk)
+        return (out == flat.to(torch.float8_e4m3fn).float()).reshape(s8.shape)
+
+    t, meta = {}, {}
+    g = torch.Generator().manual_seed(70)
+    cases = [("f32_64x64", torch.float32, (64, 64)), ("bf16_48x96", torch.bfloat16, (48, 96)),
+             ("f16_32x80", torch.float16, (32, 80)), ("bf16_16x40", torch.bfloat16, (16, 40)),
+             ("f32_8x16_zero", torch.float32, (8, 16))]
+    for name, dt, shape in cases:
+        x = (torch.randn(shape, generator=g) * torch.logspace(-2, 1, shape[-1])).to(dt)
+        if name.endswith("zero"):
+            x[0] = 0
+            x[1, :4] = -0.0
+        ga = x.float().abs().amax()
+        # the kernel loads x and computes in fp32; its final fp32 -> bf16 store in the interpreter
+        # truncates instead of rounding to nearest like the hardware cast, so the fp32 result is
+        # taken and rounded with torch's RNE cast (exact for x itself: bf16/f16 -> fp32 is exact)
+        y = hop.fp4_fake_quant_block(x.float(), ga).to(dt)
+        # which blocks' scales the interpreter casts correctly
+        xf = x.float()
+        pad = (-shape[-1]) % 16
+        xp = torch.nn.functional.pad(xf, (0, pad)) if pad else xf
+        bmax = xp.reshape(shape[0], -1, 16).abs().amax(-1)
+        gs = ga / torch.tensor(2688.0)
+        gs = torch.where(gs > 0, gs, torch.tensor(1e-12))
+        s8 = torch.minimum(bmax / (torch.tensor(6.0) * gs), torch.tensor(448.0))
+        ok = interp_cast_ok(s8)
+        t[f"{name}.x"], t[f"{name}.amax"], t[f"{name}.y"] = x, ga.reshape(1), y
+        t[f"{name}.block_ok"] = ok.to(torch.uint8)
+        meta[name] = {"blocks": int(ok.numel()), "excluded": int((~ok).sum())}
+    save_file(t, str(OUT / "nvfp4.safetensors"))
+    (OUT / "nvfp4.json").write_text(json.dumps(meta, indent=1))
+
+
 def gen_presets():
     names = [
         "INT8_DEFAULT_CFG", "INT8_WEIGHT_ONLY_CFG", "FP8_DEFAULT_CFG", "FP8_PER_CHANNEL_PER_TOKEN_CFG",
@@ -404,7 +473,7 @@ def gen_mx_kat():
 
 
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "awq", "presets", "mx_kat"]
+    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "awq", "presets", "mx_kat"]
     for s in steps:
         print("generating", s, flush=True)
         globals()["gen_" + s]()

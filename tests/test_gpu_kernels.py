@@ -376,3 +376,76 @@ def test_mse_accumulate(gpu, dtype, n):
     loss2 = torch.zeros(3, device=gpu)
     ops().mse_accumulate(a.to(gpu), b.to(gpu), loss2, 1)
     assert torch.equal(loss, loss2)
+
+
+# --------------------------------------------------------------------------------------------
+# NVFP4 (E2M1 elements, E4M3 block scales, fp32 global amax)
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(64, 128), (33, 48), (7, 40), (5, 3, 64), (1, 5)])
+def test_nvfp4_kernel_vs_oracle(gpu, dtype, shape):
+    g = torch.Generator().manual_seed(sum(shape))
+    x = (torch.randn(shape, generator=g) * torch.logspace(-3, 2, shape[-1])).to(dtype)
+    x.view(-1)[:3] = torch.tensor([0.0, -0.0, 1e-30]).to(dtype)
+    for ga in (x.float().abs().amax(), torch.tensor(0.0), x.float().abs().amax() * 100):
+        ref = R.nvfp4_fake_quant_block(x, ga)
+        out = ops().nvfp4_fake_quant_block(x.to(gpu), ga.to(gpu), 16)
+        assert same_bits(out, ref), (float(ga), mismatch(out, ref))
+
+
+def test_nvfp4_kernel_vs_reference_golden(gpu):
+    """The reference's own fp4_fake_quant_block outputs (tests/golden/nvfp4.*)."""
+    import json as _json
+    from pathlib import Path
+
+    from safetensors.torch import load_file
+
+    gold = Path(__file__).resolve().parent / "golden"
+    t = load_file(str(gold / "nvfp4.safetensors"))
+    for name in _json.loads((gold / "nvfp4.json").read_text()):
+        x, amax, y, ok = t[f"{name}.x"], t[f"{name}.amax"], t[f"{name}.y"], t[f"{name}.block_ok"].bool()
+        out = ops().nvfp4_fake_quant_block(x.to(gpu), amax.to(gpu), 16).cpu()
+        okc = ok.repeat_interleave(16, dim=1)[:, : x.shape[-1]]
+        assert torch.equal(out[okc], y[okc]), name
+        # on the excluded blocks the HIP kernel equals the oracle (hardware RNE cast)
+        assert same_bits(out, R.nvfp4_fake_quant_block(x, amax)), name
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cols", [64, 40])
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_mx_two_level_scale_vs_oracle(gpu, dtype, cols, per_channel):
+    """fused_amax_convert with E4M3 block scales and a global amax (compute_scale_with_global)."""
+    g = torch.Generator().manual_seed(cols)
+    x = (torch.randn(24, cols, generator=g) * torch.logspace(-2, 2, cols)).to(dtype)
+    ga = x.float().abs().amax(dim=1) if per_channel else x.float().abs().amax().reshape(1)
+    if per_channel and cols % 16:
+        pytest.skip("per-channel with padded blocks indexes past the rows in the reference (UB)")
+    ref = R.fused_amax_convert(x, 16, "E2M1", "E4M3", ga)
+    out = ops().fused_amax_convert(x.to(gpu), 16, R.FORMAT_CODES["E2M1"], R.FORMAT_CODES["E4M3"], ga.to(gpu))
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+def test_nvfp4_quantizer_dispatch(gpu):
+    """NVFP4 dynamic TensorQuantizer -> fp4_fake_quant_block semantics (block 16, global amax =
+    the calibrated / dynamic per-tensor amax); DISABLE_TRITON_KERNEL -> fused_amax_convert."""
+    from modelopt_amd.torch.quantization import tensor_quant as tqm
+    from modelopt_amd.torch.quantization.config import QuantizerAttributeConfig
+    from modelopt_amd.torch.quantization.nn import TensorQuantizer
+
+    cfg = QuantizerAttributeConfig(num_bits=(2, 1), block_sizes={-1: 16, "type": "dynamic", "scale_bits": (4, 3)})
+    q = TensorQuantizer(cfg).to(gpu)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(32, 64, generator=g).to(torch.bfloat16)
+    out = q(x.to(gpu))
+    ga = x.float().abs().amax()
+    assert same_bits(out, R.nvfp4_fake_quant_block(x, ga.to(torch.bfloat16).float()))
+    try:
+        tqm.DISABLE_TRITON_KERNEL = True
+        out2 = q(x.to(gpu))
+    finally:
+        tqm.DISABLE_TRITON_KERNEL = False
+    ref2 = R.fused_amax_convert(x, 16, "E2M1", "E4M3", ga.to(torch.bfloat16).float().reshape(1))
+    assert same_bits(out2, ref2), mismatch(out2, ref2)

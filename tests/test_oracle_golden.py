@@ -125,3 +125,20 @@ def test_mx_oracle_e2m1_boundaries():
     x = torch.tensor([[0.25, 0.75, 1.25, 1.75, 2.5, 3.5, 5.0, 6.0]])
     out = R.convert_to_types(x, "E2M1")
     assert out.tolist() == [[0.0, 1.0, 1.0, 2.0, 2.0, 4.0, 4.0, 6.0]]
+
+
+def test_nvfp4_oracle_matches_reference_triton_kernel():
+    """oracle.nvfp4_fake_quant_block == the reference's Triton fp4_fake_quant_block (run through
+    the Triton interpreter by tests/golden/make_golden.py) on every block whose FP8 scale the
+    interpreter casts like the hardware (see gen_nvfp4); the excluded blocks are few."""
+    from safetensors.torch import load_file
+
+    t = load_file(str(G / "nvfp4.safetensors"))
+    meta = json.loads((G / "nvfp4.json").read_text())
+    for name, m in meta.items():
+        x, amax, y, ok = t[f"{name}.x"], t[f"{name}.amax"], t[f"{name}.y"], t[f"{name}.block_ok"].bool()
+        assert m["excluded"] <= m["blocks"] // 20
+        got = R.nvfp4_fake_quant_block(x, amax)
+        rows, cols = x.shape
+        okc = ok.repeat_interleave(16, dim=1)[:, :cols]
+        assert torch.equal(got[okc], y[okc]), name
