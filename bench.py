@@ -120,6 +120,7 @@ def kernel_suite(ops, xs, steps, warmup):
         "mxfp4_block32_dynamic": (lambda x: ops.fused_amax_convert(x, 32, 6, 9, None), 4),
         "mxfp8_block32_dynamic": (lambda x: ops.fused_amax_convert(x, 32, 0, 9, None), 4),
         "int4_block128_dynamic_awq": (lambda x: ops.block_quant_dynamic(x, None, 128, 4, False, False), 4),
+        "nvfp4_block16_dynamic": (lambda x: ops.nvfp4_fake_quant_block(x, amax_t, 16), 4),
         "amax_per_tensor": (None, 2),
     }
     acc = torch.zeros(1, device="cuda")
