@@ -497,6 +497,21 @@ MXFP6_DEFAULT_CFG: dict[str, Any] = _preset(_MX((3, 2)), _MX((3, 2)), None)
 MXFP4_DEFAULT_CFG: dict[str, Any] = _preset(_MX((2, 1)), _MX((2, 1)), None)
 MXINT8_DEFAULT_CFG: dict[str, Any] = _preset(_MX(8), _MX(8), None)
 W4A8_MXFP4_FP8_CFG: dict[str, Any] = _preset(_MX((2, 1)), {"num_bits": (4, 3), "axis": None}, None)
+_NVFP4 = {"num_bits": (2, 1), "effective_bits": 4.5,
+          "block_sizes": {-1: 16, "type": "dynamic", "scale_bits": (4, 3)}}
+NVFP4_DEFAULT_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, "max")
+NVFP4_AWQ_LITE_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, "awq_lite")
+W4A8_AWQ_BETA_CFG: dict[str, Any] = _preset(
+    [{"num_bits": 4, "block_sizes": {-1: 128, "type": "static"}}, {"num_bits": (4, 3), "axis": None}],
+    {"num_bits": (4, 3), "axis": None},
+    "awq_lite",
+)
+FP8_KV_CFG: dict[str, Any] = {
+    "quant_cfg": [{"quantizer_name": "*[kv]_bmm_quantizer", "cfg": {"num_bits": (4, 3), "axis": None}}],
+}
+NVFP4_KV_CFG: dict[str, Any] = {
+    "quant_cfg": [{"quantizer_name": "*[kv]_bmm_quantizer", "cfg": copy.deepcopy(_NVFP4)}],
+}
 MXFP4_MLP_WEIGHT_ONLY_CFG: dict[str, Any] = {
     "quant_cfg": _BASE_DISABLE_ALL
     + [
@@ -521,6 +536,11 @@ __all__ += [
     "MXFP8_DEFAULT_CFG",
     "MXINT8_DEFAULT_CFG",
     "W4A8_MXFP4_FP8_CFG",
+    "NVFP4_DEFAULT_CFG",
+    "NVFP4_AWQ_LITE_CFG",
+    "W4A8_AWQ_BETA_CFG",
+    "FP8_KV_CFG",
+    "NVFP4_KV_CFG",
 ]
 
 ForwardLoop = Callable[[Any], Any]

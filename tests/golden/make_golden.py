@@ -426,7 +426,8 @@ def gen_presets():
         "INT8_DEFAULT_CFG", "INT8_WEIGHT_ONLY_CFG", "FP8_DEFAULT_CFG", "FP8_PER_CHANNEL_PER_TOKEN_CFG",
         "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG", "INT4_BLOCKWISE_WEIGHT_ONLY_CFG", "INT4_AWQ_CFG",
         "MXFP8_DEFAULT_CFG", "MXFP6_DEFAULT_CFG", "MXFP4_DEFAULT_CFG", "MXINT8_DEFAULT_CFG",
-        "W4A8_MXFP4_FP8_CFG", "MXFP4_MLP_WEIGHT_ONLY_CFG",
+        "W4A8_MXFP4_FP8_CFG", "MXFP4_MLP_WEIGHT_ONLY_CFG", "NVFP4_DEFAULT_CFG", "NVFP4_AWQ_LITE_CFG",
+        "W4A8_AWQ_BETA_CFG", "FP8_KV_CFG", "NVFP4_KV_CFG",
     ]
 
     def enc(o):
