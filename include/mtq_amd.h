@@ -157,6 +157,15 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
 int mtq_nvfp4_fake_quant(const void *x, void *y, int64_t rows, int64_t cols, int dtype,
                          const float *global_amax, int block_size, hipStream_t stream);
 
+/* Static NVFP4 element pass: x viewed as [nblocks, block] with one precomputed fp32 scale per
+ * block (already FP8-quantised by the caller): y = sign(x) * e2m1(|x| / s) * s, a zero scale gives
+ * a block of +0, a NaN/inf scale acts as 1 -- static_blockwise_fp4_fake_quant's kernel
+ * (kernels/quantization/gemm/fp4_kernel.py:193-214, nvfp4_scalar_quant in
+ * common/nvfp4_quant.py).  The per-block scale math (compute_fp4_scales, fp4_kernel.py:217-251)
+ * is a few small device ops on the host side. */
+int mtq_fp4_block_scale_quant(const void *x, void *y, int64_t nblocks, int block, int dtype,
+                              const float *scales, hipStream_t stream);
+
 /* ---- AWQ-lite search helpers ---------------------------------------------------------------
  * loss[0] += mean(float(T(a - b))^2) over n elements of dtype T: the per-alpha search loss
  * `(out - out_act).float().pow(2).mean()` (model_calib.py:1494) in one read of a and b

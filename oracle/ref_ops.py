@@ -423,6 +423,41 @@ def nvfp4_fake_quant_block(x, global_amax, block_size=16):
     return y.reshape(shape).to(dtype)
 
 
+def nvfp4_scalar_quant(x, scale):
+    """nvfp4_scalar_quant (common/nvfp4_quant.py): per-block fp32 scale broadcast over x's blocks."""
+    xf = x.float()
+    zero = scale == 0
+    safe = torch.where(zero | torch.isnan(scale) | torch.isinf(scale), torch.ones_like(scale), scale)
+    a = xf.abs() / safe
+    r = _table_round(a, "E2M1") * safe
+    y = torch.where(xf >= 0, r, -r)
+    return torch.where(zero, torch.zeros_like(y), y)
+
+
+def compute_fp4_scales(amax, global_amax=None, quantize_block_scales=True, fp8_max_for_normalization=448.0):
+    """compute_fp4_scales (fp4_kernel.py:217-251): amax/6, FP8-quantised (scaled_e4m3 ->
+    _fp8_eager) against global_amax * (448 / fp8_max) / 6 (global = max of amax if None)."""
+    scale = amax.float() / 6.0
+    if quantize_block_scales:
+        g = amax.float().amax() if global_amax is None else global_amax.float()
+        sfq = g * (448.0 / fp8_max_for_normalization) / 6.0
+        scale = fp8_eager(scale, sfq)
+    return scale
+
+
+def static_blockwise_fp4_fake_quant(x, amax, global_amax=None, quantize_block_scales=True,
+                                    fp8_max_for_normalization=448.0):
+    """Static two-level NVFP4 (kernels/quantization/gemm/fp4_kernel.py:217-316): scale = amax/6,
+    FP8-quantised (scaled_e4m3 = _fp8_eager) against global_amax * (448 / fp8_max) / 6; then
+    nvfp4_scalar_quant per block of x.numel() / amax.numel() elements."""
+    nb = amax.numel()
+    block = x.numel() // nb
+    scale = compute_fp4_scales(amax, global_amax, quantize_block_scales, fp8_max_for_normalization)
+    xb = x.reshape(nb, block)
+    y = nvfp4_scalar_quant(xb, scale.reshape(nb, 1))
+    return y.reshape(x.shape).to(x.dtype)
+
+
 # ----------------------------------------------------------------------------------------------
 # AWQ-lite helpers: restate model_calib.py:1453-1495
 # ----------------------------------------------------------------------------------------------

@@ -1057,6 +1057,44 @@ int launch_nvfp4(const T *x, T *y, int64_t rows, int64_t cols, const float *gama
   return check_launch();
 }
 
+
+// Static NVFP4 element pass with precomputed per-block scales (static_blockwise_fp4_fake_quant
+// kernel, kernels/quantization/gemm/fp4_kernel.py:193-214 -> nvfp4_scalar_quant,
+// common/nvfp4_quant.py): scale 0 -> block of +0; NaN/inf scale -> 1; y = sign * e2m1(|x|/s) * s.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void fp4_scaled_vec_kernel(const T *__restrict__ x,
+                                                                   T *__restrict__ y,
+                                                                   const float *__restrict__ sc,
+                                                                   int64_t nvec, int block) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  const float s = sc[(i * N) / block];  // block % N == 0: one scale per vector
+  const bool zero = s == 0.f;
+  const float ss = (zero || s != s || __builtin_isinf(s)) ? 1.0f : s;
+  const Nvfp4Block b{ss, 1.0f / ss};
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    v.e[j] = Elem<T>::st(zero ? 0.0f : nvfp4_qdq(Elem<T>::ld(v.e[j]), b));
+  stg_vec_nt(y + i * N, v);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void fp4_scaled_scalar_kernel(const T *__restrict__ x,
+                                                                      T *__restrict__ y,
+                                                                      const float *__restrict__ sc,
+                                                                      int64_t n, int block) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const float s = sc[i / block];
+    const bool zero = s == 0.f;
+    const float ss = (zero || s != s || __builtin_isinf(s)) ? 1.0f : s;
+    y[i] = Elem<T>::st(zero ? 0.0f : nvfp4_qdq(Elem<T>::ld(x[i]), Nvfp4Block{ss, 1.0f / ss}));
+  }
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1297,6 +1335,28 @@ int mtq_nvfp4_fake_quant(const void *x, void *y, int64_t rows, int64_t cols, int
     case 16: return launch_nvfp4<T, 16>(xt, yt, rows, cols, global_amax, stream);
     default: return launch_nvfp4<T, 32>(xt, yt, rows, cols, global_amax, stream);
     }
+  });
+}
+
+int mtq_fp4_block_scale_quant(const void *x, void *y, int64_t nblocks, int block, int dtype,
+                              const float *scales, hipStream_t stream) {
+  if (nblocks < 0 || block < 1 || (nblocks > 0 && (!x || !y || !scales))) return MTQ_ERR_INVALID_ARG;
+  if (nblocks == 0) return MTQ_OK;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    const T *xt = reinterpret_cast<const T *>(x);
+    T *yt = reinterpret_cast<T *>(y);
+    const int64_t n = nblocks * block;
+    if (block % N == 0 && aligned16(x) && aligned16(y)) {
+      const int64_t nvec = n / N;
+      fp4_scaled_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+          xt, yt, scales, nvec, block);
+    } else {
+      fp4_scaled_scalar_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(xt, yt, scales, n,
+                                                                                  block);
+    }
+    return check_launch();
   });
 }
 

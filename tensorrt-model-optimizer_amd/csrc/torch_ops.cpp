@@ -360,6 +360,24 @@ at::Tensor nvfp4_fake_quant_block(const at::Tensor &inputs, const at::Tensor &gl
   return y;
 }
 
+at::Tensor fp4_block_scale_quant(const at::Tensor &inputs, const at::Tensor &scales) {
+  check_device(inputs, "inputs");
+  const int dt = checked_dtype(inputs, "inputs");
+  TORCH_CHECK(dt != MTQ_F64, "fp4_block_scale_quant: float64 is not supported");
+  at::Tensor x = inputs.contiguous();
+  at::Tensor y = at::empty_like(x);
+  const int64_t nb = scales.numel();
+  if (x.numel() == 0) return y;
+  TORCH_CHECK(nb > 0 && x.numel() % nb == 0,
+              "fp4_block_scale_quant: x.numel() must be a multiple of scales.numel()");
+  at::Tensor s = scales.to(x.device(), at::kFloat).contiguous();
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_fp4_block_scale_quant(x.data_ptr(), y.data_ptr(), nb, (int)(x.numel() / nb), dt,
+                                     s.data_ptr<float>(), cur_stream(x));
+  check_status(st, "fp4_block_scale_quant");
+  return y;
+}
+
 at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at::Tensor> &pqs,
                                int64_t block, int64_t num_bits, bool is_unsigned,
                                bool narrow_range) {
@@ -484,6 +502,7 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("mul_cols(Tensor inputs, Tensor scale) -> Tensor");
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
   m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
+  m.def("fp4_block_scale_quant(Tensor inputs, Tensor scales) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
@@ -502,6 +521,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("mse_accumulate", &mse_accumulate);
   m.impl("mul_cols", &mul_cols);
   m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);
+  m.impl("fp4_block_scale_quant", &fp4_block_scale_quant);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
@@ -532,5 +552,6 @@ TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
   m.impl("mul_cols", [](const at::Tensor &x, const at::Tensor &) { return meta_like(x); });
   m.impl("nvfp4_fake_quant_block",
          [](const at::Tensor &x, const at::Tensor &, int64_t) { return meta_like(x); });
+  m.impl("fp4_block_scale_quant", [](const at::Tensor &x, const at::Tensor &) { return meta_like(x); });
   m.impl("mse_accumulate", [](const at::Tensor &, const at::Tensor &, at::Tensor, int64_t) {});
 }

@@ -146,6 +146,12 @@ def promote_static_block_weight_quantizers(model: nn.Module) -> int:
             if q.amax is None:
                 continue
             if q.is_nvfp4_static:
+                # two-level NVFP4: the global amax is the max of the per-block amax
+                # (reference core_utils.py:1129-1143, no shared-state groups)
+                promoted = isinstance(q, StaticBlockScaleQuantizer)
+                if not q.amax.is_meta:
+                    StaticBlockScaleQuantizer.from_tensor_quantizer(q, global_amax=q.amax.detach().float().amax())
+                    converted += 0 if promoted else 1
                 continue
             if isinstance(q._num_bits, int) and not isinstance(q, StaticBlockScaleQuantizer):
                 StaticBlockScaleQuantizer.from_tensor_quantizer(q)

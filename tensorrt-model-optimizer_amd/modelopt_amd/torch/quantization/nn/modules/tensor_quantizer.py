@@ -758,9 +758,11 @@ class TensorQuantizer(nn.Module):
 class StaticBlockScaleQuantizer(TensorQuantizer):
     """Static-block quantizer keeping fp32 per-block amax (reference :1484-1731).
 
-    The promotion after max calibration (core_utils.py:1077-1150) swaps INT static-block weight
-    quantizers to this class and keeps ``_amax`` in fp32.  The NVFP4 two-level scale path and LSQ
-    are outside the hot path."""
+    The promotion after max calibration (core_utils.py:1077-1150) swaps static-block weight
+    quantizers to this class and keeps ``_amax`` (and ``_global_amax``) in fp32.  NVFP4 static
+    weights (E2M1 + E4M3 block scales) take the two-level path: per-block scale
+    ``amax/6`` FP8-quantised against ``global_amax``, then one HIP element pass
+    (``static_blockwise_fp4_fake_quant``).  LSQ (learned scales) is outside the PTQ path."""
 
     _lsq: bool = False
     _quant_max_bound: float = 6.0
@@ -769,6 +771,9 @@ class StaticBlockScaleQuantizer(TensorQuantizer):
         amax = getattr(self, "_amax", None)
         if amax is not None and not isinstance(amax, nn.Parameter):
             self._amax = amax.to(dtype=torch.float32)
+        g = getattr(self, "_global_amax", None)
+        if g is not None and not isinstance(g, nn.Parameter) and g.dtype != torch.float32:
+            self._global_amax = g.to(dtype=torch.float32)
 
     def _amax_setter_helper(self, value):
         super()._amax_setter_helper(value)
@@ -776,20 +781,54 @@ class StaticBlockScaleQuantizer(TensorQuantizer):
 
     @classmethod
     def from_tensor_quantizer(cls, tq: TensorQuantizer, global_amax=None) -> "StaticBlockScaleQuantizer":
-        if isinstance(tq, cls):
-            tq._preserve_amax_in_fp32()
-            return tq
-        if tq.is_nvfp4_static:
-            raise NotImplementedError("modelopt_amd: NVFP4 static block scales are a 'next' item")
-        tq.__class__ = cls
-        tq._is_static_block_scale_quantizer = True
-        tq._quant_max_bound = float(tq.maxbound)
+        if not isinstance(tq, cls):
+            nvfp4 = tq.is_nvfp4_static
+            tq.__class__ = cls
+            tq._is_static_block_scale_quantizer = True
+            if nvfp4:
+                tq._is_nvfp4_static_quantizer = True
+            tq._quant_max_bound = float(tq.maxbound)
         tq._preserve_amax_in_fp32()
+        if global_amax is not None:
+            tq.global_amax = global_amax
         return tq
 
     @property
     def global_amax(self):
         return getattr(self, "_global_amax", None)
+
+    @global_amax.setter
+    def global_amax(self, value):
+        if value is None:
+            if hasattr(self, "_global_amax"):
+                self._global_amax = None
+            return
+        if not isinstance(value, torch.Tensor):
+            value = torch.tensor(value)
+        g = getattr(self, "_global_amax", None)
+        if g is None:
+            self.register_buffer("_global_amax", value.clone().detach())
+        else:
+            g.data.copy_(value.clone().detach().to(g.device))
+        self._preserve_amax_in_fp32()
+
+    @property
+    def has_quantized_block_scale(self):
+        return self._block_sizes is not None and self._block_sizes.get("scale_bits") == (4, 3)
+
+    def _fake_quantize(self, inputs):
+        if self._lsq:
+            raise NotImplementedError("modelopt_amd: LSQ is outside the PTQ path")
+        if self.amax is not None and self.is_nvfp4_static:
+            from ...tensor_quant import StaticBlockwiseFP4FakeQuantFunction, static_blockwise_fp4_fake_quant
+
+            fp8_max = 256.0 if (self._block_sizes or {}).get("four_over_six", False) else 448.0
+            if torch.is_grad_enabled() and inputs.requires_grad:
+                return StaticBlockwiseFP4FakeQuantFunction.apply(
+                    inputs, self.amax, self.global_amax, True, fp8_max, inputs.dtype, self._pass_through_bwd
+                )
+            return static_blockwise_fp4_fake_quant(inputs, self.amax, self.global_amax, True, fp8_max, inputs.dtype)
+        return super()._fake_quantize(inputs)
 
     def _apply(self, fn, recurse=True):
         amax = getattr(self, "_amax", None)
@@ -798,6 +837,9 @@ class StaticBlockScaleQuantizer(TensorQuantizer):
         if amax is not None and amax.device.type != "meta" and hasattr(self, "_amax"):
             self._amax.data.copy_(amax.to(self._amax.device, torch.float32))
         return module
+
+
+NVFP4StaticQuantizer = StaticBlockScaleQuantizer
 
 
 class SequentialQuantizer(nn.Sequential):

@@ -85,6 +85,58 @@ def fp8_fake_quant(x, amax=None):
     return quantize_op(x, amax, 8, 4, False, False)
 
 
+E4M3_MAX = 448.0
+
+
+def compute_fp4_scales(amax, global_amax=None, quantize_block_scales=True, fp8_max_for_normalization=E4M3_MAX):
+    """Per-block NVFP4 scales ``amax / 6`` optionally FP8-quantised against the global amax
+    (kernels/quantization/gemm/fp4_kernel.py:217-251): small device ops + one FP8 qdq launch."""
+    amax = amax.float()
+    scale = amax / 6.0
+    if quantize_block_scales:
+        if global_amax is None:
+            global_amax = amax.amax()  # reduce_amax(axis=None) of a non-negative amax
+        global_amax = global_amax.float()
+        scale_fp8_quant_amax = global_amax * (E4M3_MAX / fp8_max_for_normalization) / 6.0
+        scale = fp8_fake_quant(scale, scale_fp8_quant_amax)  # scaled_e4m3_impl
+    return scale
+
+
+def static_blockwise_fp4_fake_quant(
+    x, amax, global_amax=None, quantize_block_scales=True, fp8_max_for_normalization=E4M3_MAX,
+    out_dtype=None,
+):
+    """Static two-level NVFP4 fake quant (fp4_kernel.py:254-316): per-block scales from the
+    calibrated per-block ``amax`` (and the global amax), then one HIP element pass."""
+    n_blocks = amax.numel()
+    if x.numel() % n_blocks != 0:
+        raise ValueError(
+            f"x.numel() ({x.numel()}) is not divisible by amax.numel() ({n_blocks}); "
+            "they must satisfy x.numel() == NUM_FP4_BLOCKS * BLOCK_SIZE."
+        )
+    scale = compute_fp4_scales(amax, global_amax, quantize_block_scales, fp8_max_for_normalization)
+    y = _ops().fp4_block_scale_quant(x, scale.reshape(-1))
+    if out_dtype is not None and out_dtype != y.dtype:
+        y = y.to(out_dtype)
+    return y.view(x.shape)
+
+
+class StaticBlockwiseFP4FakeQuantFunction(Function):
+    """Autograd wrapper (tensor_quant.py:571-604): STE with clipping."""
+
+    @staticmethod
+    def forward(ctx, x, amax, global_amax=None, quantize_block_scales=True,
+                fp8_max_for_normalization=E4M3_MAX, out_dtype=None, pass_through_bwd=False):
+        _save_for_backward_if_needed(ctx, pass_through_bwd, x, amax)
+        return static_blockwise_fp4_fake_quant(
+            x, amax, global_amax, quantize_block_scales, fp8_max_for_normalization, out_dtype
+        )
+
+    @staticmethod
+    def backward(ctx, grad_outputs):
+        return _fake_quant_backward_function(ctx, grad_outputs, num_args=len(ctx.needs_input_grad))
+
+
 # Predefined descriptors (tensor_quant.py:279-287)
 QUANT_DESC_8BIT_PER_TENSOR = QuantizerAttributeConfig(num_bits=8)
 QUANT_DESC_UNSIGNED_8BIT_PER_TENSOR = QuantizerAttributeConfig(num_bits=8, unsigned=True)

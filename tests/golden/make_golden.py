@@ -417,6 +417,20 @@ def gen_nvfp4():
         t[f"{name}.x"], t[f"{name}.amax"], t[f"{name}.y"] = x, ga.reshape(1), y
         t[f"{name}.block_ok"] = ok.to(torch.uint8)
         meta[name] = {"blocks": int(ok.numel()), "excluded": int((~ok).sum())}
+    # static two-level path (fp4_kernel.py static_blockwise_fp4_fake_quant): its element kernel
+    # calls libdevice.isnan, which the Triton interpreter cannot run, so the golden pins the
+    # reference's scale computation (compute_fp4_scales: amax/6, FP8-quantised through the
+    # reference's scaled_e4m3_impl) -- the element pass is the same fp4_round_magnitude the
+    # dynamic golden above pins
+    fk = importlib.import_module("modelopt.torch.kernels.quantization.gemm.fp4_kernel")
+    for name, shape in [("static_scales_a", (64, 1)), ("static_scales_b", (300, 1))]:
+        amax = (torch.rand(shape, generator=g) * torch.logspace(-4, 1, shape[0]).view(-1, 1)).float()
+        amax[0] = 0.0
+        t[f"{name}.amax"] = amax
+        t[f"{name}.scale"] = fk.compute_fp4_scales(amax, amax.amax(), True, 448.0)
+        t[f"{name}.scale_g2"] = fk.compute_fp4_scales(amax, amax.amax() * 2, True, 448.0)
+        t[f"{name}.scale_46"] = fk.compute_fp4_scales(amax, None, True, 256.0)
+        meta[name] = {"static_scales": True}
     save_file(t, str(OUT / "nvfp4.safetensors"))
     (OUT / "nvfp4.json").write_text(json.dumps(meta, indent=1))
 

@@ -404,7 +404,9 @@ def test_nvfp4_kernel_vs_reference_golden(gpu):
 
     gold = Path(__file__).resolve().parent / "golden"
     t = load_file(str(gold / "nvfp4.safetensors"))
-    for name in _json.loads((gold / "nvfp4.json").read_text()):
+    for name, m in _json.loads((gold / "nvfp4.json").read_text()).items():
+        if "blocks" not in m:
+            continue
         x, amax, y, ok = t[f"{name}.x"], t[f"{name}.amax"], t[f"{name}.y"], t[f"{name}.block_ok"].bool()
         out = ops().nvfp4_fake_quant_block(x.to(gpu), amax.to(gpu), 16).cpu()
         okc = ok.repeat_interleave(16, dim=1)[:, : x.shape[-1]]
@@ -449,3 +451,52 @@ def test_nvfp4_quantizer_dispatch(gpu):
         tqm.DISABLE_TRITON_KERNEL = False
     ref2 = R.fused_amax_convert(x, 16, "E2M1", "E4M3", ga.to(torch.bfloat16).float().reshape(1))
     assert same_bits(out2, ref2), mismatch(out2, ref2)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_fp4_block_scale_quant_vs_oracle(gpu, dtype):
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(40, 32, generator=g) * 3).to(dtype)
+    scale = torch.rand(40 * 2, generator=g) * 0.5
+    scale[:4] = torch.tensor([0.0, float("nan"), float("inf"), 1e-30])
+    ref = R.nvfp4_scalar_quant(x.reshape(80, 16), scale.view(80, 1)).reshape(x.shape).to(dtype)
+    out = ops().fp4_block_scale_quant(x.to(gpu), scale.to(gpu))
+    assert same_bits(out, ref), mismatch(out, ref)
+    # ragged: block not a multiple of the vector -> scalar kernel
+    x2 = torch.randn(9, 20, generator=g).to(dtype)
+    s2 = torch.rand(9, generator=g)
+    ref2 = R.nvfp4_scalar_quant(x2, s2.view(9, 1)).to(dtype)
+    assert same_bits(ops().fp4_block_scale_quant(x2.to(gpu), s2.to(gpu)), ref2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_nvfp4_static_quantizer(gpu, dtype):
+    """NVFP4 static weight quantizer: max-calibrated per-block amax, promoted with global amax =
+    max(per-block amax) (core_utils.py:1077-1150), then the two-level static fake quant."""
+    import torch.nn as nn
+
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization.nn.modules.tensor_quantizer import StaticBlockScaleQuantizer
+
+    g = torch.Generator().manual_seed(12)
+    lin = nn.Linear(64, 48, bias=False).to(dtype)
+    with torch.no_grad():
+        lin.weight.copy_((torch.randn(48, 64, generator=g) * torch.logspace(-2, 0, 64)).to(dtype))
+    w = lin.weight.detach().clone()
+    lin.to(gpu)
+    cfg = {
+        "quant_cfg": [
+            {"quantizer_name": "*", "enable": False},
+            {"quantizer_name": "*weight_quantizer",
+             "cfg": {"num_bits": (2, 1), "block_sizes": {-1: 16, "type": "static", "scale_bits": (4, 3)}}},
+        ],
+        "algorithm": "max",
+    }
+    mtq.quantize(lin, cfg, lambda m: m(torch.randn(4, 64, device=gpu, dtype=dtype)))
+    q = lin.weight_quantizer
+    assert isinstance(q, StaticBlockScaleQuantizer)
+    amax = w.float().reshape(-1, 16).abs().amax(dim=1, keepdim=True)
+    assert torch.equal(q.amax.cpu(), amax) and torch.equal(q.global_amax.cpu(), amax.amax())
+    out = q(lin.weight)
+    ref = R.static_blockwise_fp4_fake_quant(w.reshape(-1, 16), amax, amax.amax()).reshape(w.shape)
+    assert same_bits(out, ref), mismatch(out, ref)

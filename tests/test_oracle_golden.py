@@ -136,9 +136,26 @@ def test_nvfp4_oracle_matches_reference_triton_kernel():
     t = load_file(str(G / "nvfp4.safetensors"))
     meta = json.loads((G / "nvfp4.json").read_text())
     for name, m in meta.items():
+        if "blocks" not in m:
+            continue
         x, amax, y, ok = t[f"{name}.x"], t[f"{name}.amax"], t[f"{name}.y"], t[f"{name}.block_ok"].bool()
         assert m["excluded"] <= m["blocks"] // 20
         got = R.nvfp4_fake_quant_block(x, amax)
         rows, cols = x.shape
         okc = ok.repeat_interleave(16, dim=1)[:, :cols]
         assert torch.equal(got[okc], y[okc]), name
+
+
+def test_nvfp4_static_scales_match_reference():
+    """oracle.compute_fp4_scales == the reference's compute_fp4_scales (fp4_kernel.py:217-251)."""
+    from safetensors.torch import load_file
+
+    t = load_file(str(G / "nvfp4.safetensors"))
+    meta = json.loads((G / "nvfp4.json").read_text())
+    for name, m in meta.items():
+        if not m.get("static_scales"):
+            continue
+        amax = t[f"{name}.amax"]
+        assert torch.equal(R.compute_fp4_scales(amax, amax.amax()), t[f"{name}.scale"])
+        assert torch.equal(R.compute_fp4_scales(amax, amax.amax() * 2), t[f"{name}.scale_g2"])
+        assert torch.equal(R.compute_fp4_scales(amax, None, True, 256.0), t[f"{name}.scale_46"])
