@@ -166,6 +166,29 @@ int mtq_nvfp4_fake_quant(const void *x, void *y, int64_t rows, int64_t cols, int
 int mtq_fp4_block_scale_quant(const void *x, void *y, int64_t nblocks, int block, int dtype,
                               const float *scales, hipStream_t stream);
 
+/* ---- checkpoint export (real-quant packing) ----------------------------------------------
+ * export/quant_utils.py:836-938 to_quantized_weight and the qtensor quantize() routines; weights
+ * [rows, cols] row-major of dtype, outputs raw bytes.
+ *  mtq_export_fp8:   y = e4m3(w / scale) as torch's float8_e4m3fn cast (RNE, |v| > 464 -> NaN);
+ *                    per_row: scale[rows] (fp32 quotient), else scale[0] with the quotient first
+ *                    rounded to dtype when round_to_dtype (bf16 / 0-dim fp32 stays bf16 in torch).
+ *  mtq_export_int4:  pack_int4_in_uint8 (:792-833): q = clamp(rint(w / scale[r, c/block]), -8, 7),
+ *                    rows 2i and 2i+1 share byte y[i, c] (low nibble = even row); rows even.
+ *  mtq_export_nvfp4: NVFP4QTensor.quantize (qtensor/nvfp4_tensor.py:253-342): code of
+ *                    w / (block_scale[r, c/block] * scale_2[0]) (E2M1 RNE, sign bit), columns 2j
+ *                    and 2j+1 share y[r, j] (low = even); block_scale holds the fp8 scales as fp32.
+ *  mtq_export_mxfp4: MXFP4QTensor.quantize (qtensor/mxfp4_tensor.py:38-81): per `block` elements
+ *                    an E8M0 exponent byte in scales[n/block] and packed codes in y[n/2]. */
+int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype,
+                   const float *scale, int per_row, int round_to_dtype, hipStream_t stream);
+int mtq_export_int4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype,
+                    const float *scale, int block, hipStream_t stream);
+int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype,
+                     const float *block_scale, const float *scale_2, int block,
+                     hipStream_t stream);
+int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int dtype, int block,
+                     hipStream_t stream);
+
 /* ---- AWQ-lite search helpers ---------------------------------------------------------------
  * loss[0] += mean(float(T(a - b))^2) over n elements of dtype T: the per-alpha search loss
  * `(out - out_act).float().pow(2).mean()` (model_calib.py:1494) in one read of a and b

@@ -1095,6 +1095,146 @@ __global__ __launch_bounds__(kThreads) void fp4_scaled_scalar_kernel(const T *__
   }
 }
 
+
+// ============================================================================================
+// Real-quant packing for checkpoint export (export/quant_utils.py to_quantized_weight and the
+// qtensor quantize() routines).  All HBM-bound byte work: one read of the weight, one write of
+// the packed bytes.
+// ============================================================================================
+// torch float -> float8_e4m3fn byte: RNE, |v| > 464 or NaN/inf -> NaN (0x7F | sign); the
+// 448..464 band rounds to 448.
+__device__ __forceinline__ uint32_t e4m3_byte(float v) {
+  const uint32_t sign = (__float_as_uint(v) >> 24) & 0x80u;
+  if (v != v || fabsf(v) > 464.0f) return 0x7Fu | sign;
+  const float c = v > 448.f ? 448.f : (v < -448.f ? -448.f : v);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xFFu;
+}
+
+// weight / scale -> e4m3 bytes.  per_row: scale[row] (the division then happens in fp32, as torch
+// promotes bf16 / fp32[rows, 1] to fp32); per-tensor: scale[0] and, with round_dtype, the quotient
+// is first rounded to the weight dtype (torch keeps bf16 / 0-dim fp32 in bf16).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_fp8_kernel(const T *__restrict__ x,
+                                                               uint8_t *__restrict__ y, int64_t n,
+                                                               int64_t cols,
+                                                               const float *__restrict__ scale,
+                                                               int per_row, int round_dtype) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const float s = scale[per_row ? i / cols : 0];
+    float q = div_rn(Elem<T>::ld(x[i]), s, 1.0f / s);
+    if (round_dtype) q = Elem<T>::ld(Elem<T>::st(q));
+    y[i] = (uint8_t)e4m3_byte(q);
+  }
+}
+
+// INT4 AWQ: q = clamp(rint(w / scale[row, col / block]), -8, 7); two consecutive ROWS share a
+// byte (low nibble = even row): y[r/2, c] (pack_int4_in_uint8, export/quant_utils.py:792-833).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_int4_kernel(const T *__restrict__ x,
+                                                                uint8_t *__restrict__ y,
+                                                                int64_t prow_count, int64_t cols,
+                                                                const float *__restrict__ scale,
+                                                                int64_t nblk, int block) {
+  const int64_t n = prow_count * cols;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const int64_t pr = i / cols, c = i - pr * cols;
+    uint32_t out = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t r = 2 * pr + h;
+      const float s = scale[r * nblk + c / block];
+      float q = __builtin_rintf(div_rn(Elem<T>::ld(x[r * cols + c]), s, 1.0f / s));
+      q = q < -8.f ? -8.f : (q > 7.f ? 7.f : q);  // NaN stays NaN -> int8 cast below
+      const int v = q != q ? 0 : (int)q;
+      out |= ((uint32_t)v & 0xFu) << (4 * h);
+    }
+    y[i] = (uint8_t)out;
+  }
+}
+
+// E2M1 code (sign << 3 | magnitude index) the way NVFP4QTensor._cast_fp4 computes it:
+// searchsorted(right=False) over the midpoints + 1 on the odd midpoints (ties to even index);
+// NaN -> 7, the sign bit from (v < 0).
+__device__ __forceinline__ uint32_t nvfp4_code(float q) {
+  const float a = fabsf(q);
+  uint32_t ord;
+  if (a != a) {
+    ord = 7;
+  } else {
+    ord = (a > 0.25f) + (a > 0.75f) + (a > 1.25f) + (a > 1.75f) + (a > 2.5f) + (a > 3.5f) + (a > 5.0f);
+    ord += (a == 0.75f) | (a == 1.75f) | (a == 3.5f);
+  }
+  return ((q < 0.f) ? 8u : 0u) + ord;
+}
+
+// NVFP4QTensor.quantize (qtensor/nvfp4_tensor.py:253-342): q = w / (fp32(scale_fp8[blk]) * s2),
+// packed two per byte along the last dim (low nibble = even column).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_nvfp4_kernel(const T *__restrict__ x,
+                                                                 uint8_t *__restrict__ y,
+                                                                 int64_t npairs, int64_t cols,
+                                                                 const float *__restrict__ sblk,
+                                                                 const float *__restrict__ s2,
+                                                                 int block) {
+  const float g = *s2;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int64_t nb_row = cols / block;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < npairs; i += stride) {
+    const int64_t e0 = 2 * i;
+    const int64_t row = e0 / cols, c = e0 - row * cols;  // cols even: a pair never straddles rows
+    const float d = sblk[row * nb_row + c / block] * g;
+    const float r = 1.0f / d;
+    const uint32_t lo = nvfp4_code(div_rn(Elem<T>::ld(x[e0]), d, r));
+    const uint32_t hi = nvfp4_code(div_rn(Elem<T>::ld(x[e0 + 1]), d, r));
+    y[i] = (uint8_t)(lo | (hi << 4));
+  }
+}
+
+// MXFP4QTensor.quantize (qtensor/mxfp4_tensor.py:38-81): per block of `block` along the flat
+// tensor, e = ceil(max(log2(amax / 6), -127)) (log2 correctly rounded to fp32), q = w / 2^e,
+// code = #(bounds < |q|) (ties toward zero) + 8 * (sign(q) <= 0) -- zero encodes with the sign bit
+// set, as torch.sign gives 0 there; bytes pack (even, odd) into (low, high); scale byte e + 127.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_mxfp4_kernel(const T *__restrict__ x,
+                                                                 uint8_t *__restrict__ y,
+                                                                 uint8_t *__restrict__ sc,
+                                                                 int64_t nblocks, int block) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x; b < nblocks; b += stride) {
+    const T *xb = x + b * block;
+    float amax = 0.f;
+    for (int k = 0; k < block; ++k) {
+      const float a = fabsf(Elem<T>::ld(xb[k]));
+      amax = (a > amax || a != a) ? a : amax;  // torch.max propagates NaN
+    }
+    const float descale = amax / 6.0f;
+    float e;
+    if (descale != descale) {
+      e = descale;
+    } else {
+      const float l2 = descale > 0.f ? (float)log2((double)descale) : -INFINITY;
+      e = __builtin_ceilf(l2 > -127.f ? l2 : -127.f);
+    }
+    sc[b] = (uint8_t)(int)(e + 127.f);
+    const float p = (e == e) ? exp2f(e) : e;
+    for (int k = 0; k < block; k += 2) {
+      uint32_t code[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float q = Elem<T>::ld(xb[k + h]) / p;
+        const float a = fabsf(q);
+        const uint32_t ord = (a > 0.25f) + (a > 0.75f) + (a > 1.25f) + (a > 1.75f) + (a > 2.5f) +
+                             (a > 3.5f) + (a > 5.0f);
+        const uint32_t sb = (q > 0.f) ? 0u : 1u;  // sign(q) in {1, 0, -1, NaN}: (2 - sign) // 2
+        code[h] = sb * 8u + ord;
+      }
+      y[(b * block + k) / 2] = (uint8_t)((code[0] & 0xFFu) + ((code[1] << 4) & 0xFFu));
+    }
+  }
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1356,6 +1496,62 @@ int mtq_fp4_block_scale_quant(const void *x, void *y, int64_t nblocks, int block
       fp4_scaled_scalar_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(xt, yt, scales, n,
                                                                                   block);
     }
+    return check_launch();
+  });
+}
+
+int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype,
+                   const float *scale, int per_row, int round_to_dtype, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || (rows * cols > 0 && (!x || !y || !scale))) return MTQ_ERR_INVALID_ARG;
+  if (rows * cols == 0) return MTQ_OK;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    const int64_t n = rows * cols;
+    export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), y, n, cols, scale, per_row, round_to_dtype);
+    return check_launch();
+  });
+}
+
+int mtq_export_int4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype,
+                    const float *scale, int block, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || rows % 2 || block < 1 || cols % block) return MTQ_ERR_INVALID_ARG;
+  if (rows * cols == 0) return MTQ_OK;
+  if (!x || !y || !scale) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    const int64_t n = rows / 2 * cols;
+    export_int4_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), y, rows / 2, cols, scale, cols / block, block);
+    return check_launch();
+  });
+}
+
+int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype,
+                     const float *block_scale, const float *scale_2, int block,
+                     hipStream_t stream) {
+  if (rows < 0 || cols < 0 || cols % 2 || block < 2 || cols % block) return MTQ_ERR_INVALID_ARG;
+  if (rows * cols == 0) return MTQ_OK;
+  if (!x || !y || !block_scale || !scale_2) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    const int64_t npairs = rows * cols / 2;
+    export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), y, npairs, cols, block_scale, scale_2, block);
+    return check_launch();
+  });
+}
+
+int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int dtype, int block,
+                     hipStream_t stream) {
+  if (n < 0 || block < 2 || block % 2 || n % block) return MTQ_ERR_INVALID_ARG;
+  if (n == 0) return MTQ_OK;
+  if (!x || !y || !scales) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    const int64_t nb = n / block;
+    export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), y, scales, nb, block);
     return check_launch();
   });
 }

@@ -17,6 +17,7 @@
 #include <map>
 #include <mutex>
 #include <utility>
+#include <tuple>
 #include <vector>
 
 #include "mtq_amd.h"
@@ -378,6 +379,79 @@ at::Tensor fp4_block_scale_quant(const at::Tensor &inputs, const at::Tensor &sca
   return y;
 }
 
+// ---- checkpoint export packing ---------------------------------------------------------------
+at::Tensor export_fp8(const at::Tensor &weight, const at::Tensor &scale, bool per_row,
+                      bool round_to_dtype) {
+  check_device(weight, "weight");
+  const int dt = checked_dtype(weight, "weight");
+  TORCH_CHECK(dt != MTQ_F64, "export_fp8: float64 is not supported");
+  at::Tensor x = weight.contiguous();
+  const int64_t cols = x.dim() == 0 ? 1 : x.size(-1);
+  const int64_t rows = cols ? x.numel() / cols : 0;
+  at::Tensor s = scale.to(x.device(), at::kFloat).contiguous();
+  TORCH_CHECK(per_row ? s.numel() == rows : s.numel() == 1, "export_fp8: scale shape");
+  at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_export_fp8(x.data_ptr(), y.data_ptr<uint8_t>(), rows, cols, dt,
+                              s.data_ptr<float>(), per_row, round_to_dtype, cur_stream(x)),
+               "export_fp8");
+  return y.view(at::kFloat8_e4m3fn);
+}
+
+at::Tensor export_int4(const at::Tensor &weight, const at::Tensor &scale) {
+  check_device(weight, "weight");
+  const int dt = checked_dtype(weight, "weight");
+  TORCH_CHECK(dt != MTQ_F64 && weight.dim() == 2, "export_int4: 2-D f32/f16/bf16 weight expected");
+  at::Tensor x = weight.contiguous();
+  at::Tensor s = scale.to(x.device(), at::kFloat).contiguous();
+  const int64_t rows = x.size(0), cols = x.size(1);
+  TORCH_CHECK(s.dim() == 2 && s.size(0) == rows && cols % s.size(1) == 0, "export_int4: scale shape");
+  at::Tensor y = at::empty({rows / 2, cols}, x.options().dtype(at::kByte));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_export_int4(x.data_ptr(), y.data_ptr<uint8_t>(), rows, cols, dt,
+                               s.data_ptr<float>(), (int)(cols / s.size(1)), cur_stream(x)),
+               "export_int4");
+  return y;
+}
+
+at::Tensor export_nvfp4(const at::Tensor &weight, const at::Tensor &block_scale,
+                        const at::Tensor &scale_2) {
+  check_device(weight, "weight");
+  const int dt = checked_dtype(weight, "weight");
+  TORCH_CHECK(dt != MTQ_F64, "export_nvfp4: float64 is not supported");
+  at::Tensor x = weight.contiguous();
+  const int64_t cols = x.size(-1), rows = x.numel() / cols;
+  at::Tensor bs = block_scale.to(x.device(), at::kFloat).contiguous();
+  at::Tensor s2 = scale_2.to(x.device(), at::kFloat).contiguous();
+  TORCH_CHECK(bs.numel() > 0 && x.numel() % bs.numel() == 0 && s2.numel() == 1,
+              "export_nvfp4: scale shapes");
+  const int block = (int)(x.numel() / bs.numel());
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = cols / 2;
+  at::Tensor y = at::empty(shape, x.options().dtype(at::kByte));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_export_nvfp4(x.data_ptr(), y.data_ptr<uint8_t>(), rows, cols, dt,
+                                bs.data_ptr<float>(), s2.data_ptr<float>(), block, cur_stream(x)),
+               "export_nvfp4");
+  return y;
+}
+
+std::tuple<at::Tensor, at::Tensor> export_mxfp4(const at::Tensor &weight, int64_t block) {
+  check_device(weight, "weight");
+  const int dt = checked_dtype(weight, "weight");
+  TORCH_CHECK(dt != MTQ_F64, "export_mxfp4: float64 is not supported");
+  at::Tensor x = weight.contiguous();
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = shape.back() / 2;
+  at::Tensor y = at::empty(shape, x.options().dtype(at::kByte));
+  at::Tensor sc = at::empty({x.numel() / block, 1}, x.options().dtype(at::kByte));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_export_mxfp4(x.data_ptr(), y.data_ptr<uint8_t>(), sc.data_ptr<uint8_t>(),
+                                x.numel(), dt, (int)block, cur_stream(x)),
+               "export_mxfp4");
+  return {y, sc};
+}
+
 at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at::Tensor> &pqs,
                                int64_t block, int64_t num_bits, bool is_unsigned,
                                bool narrow_range) {
@@ -503,6 +577,10 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
   m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
   m.def("fp4_block_scale_quant(Tensor inputs, Tensor scales) -> Tensor");
+  m.def("export_fp8(Tensor weight, Tensor scale, bool per_row, bool round_to_dtype) -> Tensor");
+  m.def("export_int4(Tensor weight, Tensor scale) -> Tensor");
+  m.def("export_nvfp4(Tensor weight, Tensor block_scale, Tensor scale_2) -> Tensor");
+  m.def("export_mxfp4(Tensor weight, int block) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
@@ -522,6 +600,10 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("mul_cols", &mul_cols);
   m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);
   m.impl("fp4_block_scale_quant", &fp4_block_scale_quant);
+  m.impl("export_fp8", &export_fp8);
+  m.impl("export_int4", &export_int4);
+  m.impl("export_nvfp4", &export_nvfp4);
+  m.impl("export_mxfp4", &export_mxfp4);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {

@@ -30,15 +30,28 @@ def quantizer_attr_names(weight_name: str = "weight") -> QuantizerAttrNames:
     )
 
 
-def weight_attr_names(module: nn.Module):
-    """Names of the quantized weight parameters of a converted module (non-recursive)."""
+def representative_weight_quantizer(module: nn.Module, weight_name: str = "weight"):
+    """The weight quantizer of ``weight_name``: singular ``<name>_weight_quantizer``, or the first
+    of a fused-experts plural ``<name>_weight_quantizers`` ModuleList (reference core_utils.py:215)."""
     from ..nn.modules.tensor_quantizer import SequentialQuantizer, TensorQuantizer
 
+    q = module._modules.get(quantizer_attr_names(weight_name).weight_quantizer)
+    if isinstance(q, (TensorQuantizer, SequentialQuantizer)):
+        return q
+    plural = module._modules.get(quantizer_attr_names(weight_name).weight_quantizer + "s")
+    if isinstance(plural, nn.ModuleList) and len(plural) > 0:
+        first = plural[0]
+        if isinstance(first, (TensorQuantizer, SequentialQuantizer)):
+            return first
+    return None
+
+
+def weight_attr_names(module: nn.Module):
+    """Names of the quantized weight parameters of a converted module (non-recursive)."""
     for name, p in module._parameters.items():
         if p is None:
             continue
-        q = module._modules.get(quantizer_attr_names(name).weight_quantizer)
-        if isinstance(q, (TensorQuantizer, SequentialQuantizer)):
+        if representative_weight_quantizer(module, name) is not None:
             yield name
 
 

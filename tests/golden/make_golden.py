@@ -435,6 +435,75 @@ def gen_nvfp4():
     (OUT / "nvfp4.json").write_text(json.dumps(meta, indent=1))
 
 
+def tiny_llama_export():
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    cfg = LlamaConfig(
+        hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+        num_key_value_heads=2, vocab_size=32, max_position_embeddings=64,
+        architectures=["LlamaForCausalLM"],
+    )
+    torch.manual_seed(80)
+    return LlamaForCausalLM(cfg).eval()
+
+
+EXPORT_CASES = {
+    "fp8": "FP8_DEFAULT_CFG",
+    "fp8_pcpt": "FP8_PER_CHANNEL_PER_TOKEN_CFG",
+    "int8_sq": "INT8_DEFAULT_CFG",
+    "int4_awq": "INT4_AWQ_CFG",
+    "w4a8_awq": "W4A8_AWQ_BETA_CFG",
+    "nvfp4": "NVFP4_DEFAULT_CFG",
+    "mxfp4": "MXFP4_DEFAULT_CFG",
+}
+
+
+def export_cfg(name):
+    """The preset, with INT4 groups of 32 so the tiny model (hidden 64) has two per row."""
+    import copy
+
+    cfg = copy.deepcopy(getattr(mtq, EXPORT_CASES[name]))
+    for e in cfg["quant_cfg"]:
+        if e.get("quantizer_name") == "*weight_quantizer":
+            c = e["cfg"]
+            first = c[0] if isinstance(c, list) else c
+            if first.get("num_bits") == 4:
+                first["block_sizes"] = {-1: 32, "type": "static"}
+    return cfg
+
+
+def gen_export():
+    """Unified HF checkpoint export (export/unified_export_hf.py export_hf_checkpoint) of a tiny
+    Llama per format: the post-calibration state (weights + quantizer buffers) and the exported
+    files (model.safetensors tensors, hf_quant_config.json, config.json quantization_config)."""
+    import tempfile
+
+    from safetensors.torch import load_file
+
+    from modelopt.torch.export import export_hf_checkpoint
+
+    g = torch.Generator().manual_seed(81)
+    ids = torch.randint(0, 32, (4, 2, 16), generator=g)
+    t, meta = {"calib_ids": ids}, {}
+    for name in EXPORT_CASES:
+        m = tiny_llama_export()
+        mtq.quantize(m, export_cfg(name), lambda mm: [mm(b) for b in ids])
+        for k, v in m.state_dict().items():
+            t[f"{name}.state.{k}"] = v.detach().clone().contiguous()
+        with tempfile.TemporaryDirectory() as d:
+            export_hf_checkpoint(m, export_dir=d)
+            for k, v in load_file(os.path.join(d, "model.safetensors")).items():
+                t[f"{name}.export.{k}"] = v.contiguous()
+            hq = json.load(open(os.path.join(d, "hf_quant_config.json")))
+            cq = json.load(open(os.path.join(d, "config.json"))).get("quantization_config")
+        hq["producer"]["version"] = None
+        if cq and "producer" in cq:
+            cq["producer"]["version"] = None
+        meta[name] = {"preset": EXPORT_CASES[name], "hf_quant_config": hq, "quantization_config": cq}
+    save_file(t, str(OUT / "export.safetensors"))
+    (OUT / "export.json").write_text(json.dumps(meta, indent=1))
+
+
 def gen_presets():
     names = [
         "INT8_DEFAULT_CFG", "INT8_WEIGHT_ONLY_CFG", "FP8_DEFAULT_CFG", "FP8_PER_CHANNEL_PER_TOKEN_CFG",
@@ -488,7 +557,7 @@ def gen_mx_kat():
 
 
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "awq", "presets", "mx_kat"]
+    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "export", "awq", "presets", "mx_kat"]
     for s in steps:
         print("generating", s, flush=True)
         globals()["gen_" + s]()

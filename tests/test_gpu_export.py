@@ -1,0 +1,75 @@
+"""Unified HF checkpoint export vs the reference's own export (tests/golden/export.*).
+
+For each format the reference quantized a tiny Llama (hidden 64) on the CPU and exported it; the
+golden holds its post-calibration state (weights + quantizer buffers) and the exported tensors
+and configs.  Here the same model is converted with modelopt_amd, the reference's
+post-calibration state is loaded (so calibration differences cannot leak in), and
+export_hf_checkpoint must reproduce every exported tensor bit for bit and both JSON configs.
+"""
+
+import copy
+import json
+import os
+from pathlib import Path
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+META = json.loads((G / "export.json").read_text())
+
+
+def _tiny():
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=32, max_position_embeddings=64,
+                      architectures=["LlamaForCausalLM"])
+    torch.manual_seed(80)
+    return LlamaForCausalLM(cfg).eval()
+
+
+def _cfg(mtq, preset):
+    cfg = copy.deepcopy(getattr(mtq, preset))
+    for e in cfg["quant_cfg"]:
+        if e.get("quantizer_name") == "*weight_quantizer":
+            c = e["cfg"]
+            first = c[0] if isinstance(c, list) else c
+            if first.get("num_bits") == 4:
+                first["block_sizes"] = {-1: 32, "type": "static"}
+    return cfg
+
+
+@pytest.mark.parametrize("case", sorted(META))
+def test_export_matches_reference(gpu, case, tmp_path):
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.export import export_hf_checkpoint
+
+    t = load_file(str(G / "export.safetensors"))
+    ids = t["calib_ids"].to(gpu)
+    model = _tiny().to(gpu)
+    mtq.quantize(model, _cfg(mtq, META[case]["preset"]), lambda m: [m(b) for b in ids])
+    state = {k[len(case) + 7:]: v for k, v in t.items() if k.startswith(case + ".state.")}
+    missing, unexpected = model.load_state_dict(state, strict=False)
+    assert not unexpected, unexpected
+    assert not [k for k in missing if "quantizer" not in k], missing
+    export_hf_checkpoint(model, export_dir=str(tmp_path))
+    got = load_file(str(tmp_path / "model.safetensors"))
+    want = {k[len(case) + 8:]: v for k, v in t.items() if k.startswith(case + ".export.")}
+    assert set(got) == set(want), (sorted(set(got) ^ set(want)))[:10]
+    bad = []
+    for k, v in want.items():
+        g = got[k]
+        if g.dtype != v.dtype or g.shape != v.shape:
+            bad.append((k, g.dtype, v.dtype, tuple(g.shape), tuple(v.shape)))
+        elif not torch.equal(g.view(torch.uint8) if g.element_size() == 1 else g, v.view(torch.uint8) if v.element_size() == 1 else v):
+            bad.append((k, "values"))
+    assert not bad, bad[:8]
+    hq = json.loads((tmp_path / "hf_quant_config.json").read_text())
+    hq["producer"]["version"] = None
+    assert hq == META[case]["hf_quant_config"]
+    cq = json.loads((tmp_path / "config.json").read_text())["quantization_config"]
+    cq["producer"]["version"] = None
+    assert cq == META[case]["quantization_config"]
