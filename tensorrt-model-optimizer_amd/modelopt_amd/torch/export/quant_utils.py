@@ -51,6 +51,25 @@ E2M1_MAX = 6.0
 E4M3_MAX = 448.0
 
 
+def _div(t: torch.Tensor, c) -> torch.Tensor:
+    """IEEE fp32 ``t / c``.  torch on ROCm turns a division by a host scalar into a multiply by
+    its reciprocal (1-ulp off the reference's CPU export); a device-tensor divisor is a true
+    division."""
+    t = t.float()
+    if not isinstance(c, torch.Tensor):
+        c = torch.tensor(float(c), dtype=torch.float32, device=t.device)
+    return torch.div(t, c.to(device=t.device, dtype=torch.float32))
+
+
+def _mean0(ts: list[torch.Tensor]) -> torch.Tensor:
+    """torch.mean(torch.stack(ts), 0) as the CPU computes it for a few rows: a sequential fp32
+    sum, then one true division."""
+    acc = ts[0].float()
+    for t in ts[1:]:
+        acc = acc + t.float()
+    return _div(acc, len(ts)).to(ts[0].dtype)
+
+
 def _fp8_max_for_normalization(quantizer) -> float:
     bs = getattr(quantizer, "block_sizes", None) or {}
     return 256.0 if bool(bs.get("four_over_six", False)) else E4M3_MAX
@@ -142,14 +161,14 @@ def nvfp4_weights_scaling_factor_2_from_quantizer(wq) -> torch.Tensor:
     m = _fp8_max_for_normalization(wq)
     g = _static_global_amax(wq)
     if g is not None:
-        return g.float() / (E2M1_MAX * m)
+        return _div(g, E2M1_MAX * m)
     assert hasattr(wq, "_amax"), "Weight quantizer does not have attribute amax"
-    return wq._amax.float() / (E2M1_MAX * m)
+    return _div(wq._amax, E2M1_MAX * m)
 
 
 def _cast_per_block_scale_to_fp8(scale, scale_max=None, fp8_max=E4M3_MAX):
     if scale_max is not None:
-        scale = scale.float() * fp8_max / scale_max
+        scale = _div(scale.float() * fp8_max, scale_max)
     return scale.clamp(min=2**-9, max=E4M3_MAX).to(torch.float8_e4m3fn)
 
 
@@ -159,7 +178,7 @@ def nvfp4_weights_scaling_factor(weight, block_size, scale_2, keep_high_precisio
         "Weight shape is not divisible for block size for block quantization."
     )
     per_block_amax = weight.reshape(*weight.shape[:-1], -1, block_size).abs().amax(dim=-1).float()
-    per_block_scale = per_block_amax / (E2M1_MAX * scale_2.to(per_block_amax.device))
+    per_block_scale = _div(per_block_amax, E2M1_MAX * scale_2.to(per_block_amax.device).float())
     per_block_scale[per_block_scale == 0] = 1.0
     if not keep_high_precision:
         per_block_scale = _cast_per_block_scale_to_fp8(per_block_scale)
@@ -173,8 +192,8 @@ def nvfp4_weights_scaling_factor_from_quantizer(wq, weight, scale_2=None, keep_h
         scale_2 = nvfp4_weights_scaling_factor_2_from_quantizer(wq)
     g = _static_global_amax(wq)
     if g is not None:
-        per_block_scale_max = g.float() / E2M1_MAX
-        per_block_scale = wq._amax.float() / E2M1_MAX
+        per_block_scale_max = _div(g, E2M1_MAX)
+        per_block_scale = _div(wq._amax, E2M1_MAX)
         per_block_scale[per_block_scale == 0] = 1.0
         per_block_scale = per_block_scale.view(*weight.shape[:-1], weight.shape[-1] // block_size)
         if not keep_high_precision:
@@ -196,7 +215,7 @@ def get_scaling_factor(quantizer: TensorQuantizer) -> torch.Tensor | None:
     if quantizer.num_bits == (2, 1):
         sf = nvfp4_weights_scaling_factor_2_from_quantizer(quantizer)
     else:
-        sf = amax.float() / quantizer.maxbound
+        sf = _div(amax, quantizer.maxbound)
     assert torch.all(sf > 0), f"scaling factor {sf} not positive."
     return sf
 
@@ -211,7 +230,7 @@ def get_activation_scaling_factor(module, input_quantizer_name="input_quantizer"
         amax = iq.export_amax()
         if amax is None:
             return None
-        sf = amax.float() / (iq.maxbound * E4M3_MAX)
+        sf = _div(amax, iq.maxbound * E4M3_MAX)
         assert torch.all(sf > 0), f" activation scaling factor {sf} not positive."
         return sf
     return get_scaling_factor(iq)
@@ -227,7 +246,7 @@ def get_weight_scaling_factor(module, weight_name="weight"):
     fmt = get_quantization_format(module)
     if fmt in NVFP4_FAMILY:
         if fmt == QUANTIZATION_W4A8_NVFP4_FP8:
-            s2 = wq._amax.float() / 448.0
+            s2 = _div(wq._amax, 448.0)
         else:
             s2 = nvfp4_weights_scaling_factor_2_from_quantizer(wq)
         return nvfp4_weights_scaling_factor_from_quantizer(wq, weight, s2.to(weight.device))
@@ -244,7 +263,7 @@ def get_weight_scaling_factor_2(module, weight_name="weight"):
     fmt = get_quantization_format(module)
     if fmt in NVFP4_FAMILY:
         if fmt == QUANTIZATION_W4A8_NVFP4_FP8:
-            return wq._amax.float() / 448.0
+            return _div(wq._amax, 448.0)
         return nvfp4_weights_scaling_factor_2_from_quantizer(wq)
     if not isinstance(wq, SequentialQuantizer) or not wq[-1].is_enabled:
         return None
@@ -338,7 +357,7 @@ def preprocess_linear_fusion(modules: list[nn.Module], resmooth_only=False):
     assert all(f == fmts[0] for f in fmts), "Modules have different quantization formats"
     if hasattr(modules[0], "input_quantizer"):
         if modules[0].input_quantizer.pre_quant_scale is not None:
-            avg = torch.mean(torch.stack([m.input_quantizer.pre_quant_scale for m in modules]), dim=0)
+            avg = _mean0([m.input_quantizer.pre_quant_scale for m in modules])
             for m in modules:
                 if not torch.equal(m.input_quantizer.pre_quant_scale, avg):
                     _update_pre_quant_scale(m, avg)
@@ -417,7 +436,8 @@ def fuse_prequant_to_linear(model: nn.Module, fuse_grouped_heads=False):
                 nkv = module.config.num_key_value_heads
                 hd = into.weight.shape[0] // nkv
                 n_rep = pqs.numel() // nkv // hd
-                avg = pqs.view(nkv, n_rep, hd).mean(dim=1)
+                v = pqs.view(nkv, n_rep, hd)
+                avg = _mean0([v[:, j] for j in range(n_rep)])
                 _update_pre_quant_scale(frm, avg.unsqueeze(1).expand(nkv, n_rep, hd).reshape(-1))
                 pqs = avg.reshape(-1)
             into.weight = nn.Parameter(into.weight * pqs.view(-1, 1))

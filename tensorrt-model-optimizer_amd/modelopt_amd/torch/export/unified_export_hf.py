@@ -40,6 +40,7 @@ from .model_config import (
     QUANTIZATION_W4A8_AWQ,
 )
 from .quant_utils import (
+    _div,
     fuse_prequant_layernorm,
     fuse_prequant_to_linear,
     get_activation_scaling_factor,
@@ -164,7 +165,7 @@ def _export_quantized_weight(sub_module: nn.Module, dtype: torch.dtype, weight_n
         if wq._amax.dim() == 1:
             wsf = torch.tensor(wq.amax.item() / wq.maxbound)
         else:
-            wsf = (wq.amax / wq.maxbound).clone().detach()
+            wsf = _div(wq.amax, wq.maxbound).clone().detach()
         sub_module.register_buffer(names.weight_scale, wsf)
         if hasattr(iq, "_amax"):
             iq._amax = iq._amax.to(torch.float32)

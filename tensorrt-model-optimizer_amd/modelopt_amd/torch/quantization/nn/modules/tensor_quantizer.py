@@ -125,9 +125,12 @@ class TensorQuantizer(nn.Module):
     # ---- configuration --------------------------------------------------------------------
     def set_from_attribute_config(self, attribute_cfg: QuantizerAttributeConfig | dict[str, Any]):
         """Set quantizer attributes from attribute_cfg (reference :228-290)."""
-        if isinstance(attribute_cfg, dict):
+        if isinstance(attribute_cfg, dict) and set(attribute_cfg) == {"enable"}:
+            # a bare enable toggle (set_quantizer_by_cfg enable entries, contexts): the reference
+            # applies dict attributes unvalidated, so {"enable": True} is legal here
+            items = attribute_cfg.items()
+        elif isinstance(attribute_cfg, dict):
             # validate like the reference (pydantic) but apply only the keys that were given
-            QuantizerAttributeConfig(**attribute_cfg)
             items = QuantizerAttributeConfig.model_validate(attribute_cfg).model_dump(
                 include=set(attribute_cfg.keys())
             ).items()
