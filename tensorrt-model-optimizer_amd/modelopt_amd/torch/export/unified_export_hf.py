@@ -17,6 +17,7 @@ MXFP4 nibble pairs) with ``weight_scale`` / ``weight_scale_2`` / ``input_scale``
 from __future__ import annotations
 
 import copy
+import importlib
 import json
 import re
 import warnings
@@ -30,6 +31,12 @@ from ..quantization.conversion import set_quantizer_by_cfg_context
 from ..quantization.nn import SequentialQuantizer, TensorQuantizer
 from ..quantization.utils.names import is_quantized_linear, quantizer_attr_names
 from .convert_hf_config import convert_hf_quant_config_format
+from .quant_aware_conversion import (
+    QuantConversionUnsupportedError,
+    build_reverse_name_mapper,
+    revert_quant_config_names,
+    revert_weight_conversion_quant_aware,
+)
 from .model_config import (
     NVFP4_FAMILY,
     QUANTIZATION_FP8,
@@ -295,10 +302,32 @@ def export_hf_checkpoint(model, dtype: torch.dtype | None = None, export_dir="/t
     export_dir.mkdir(parents=True, exist_ok=True)
     post_state, hf_quant_config = _export_transformers_checkpoint(model, dtype)
     state = {**post_state, **(extra_state_dict or {})}
+    # back to the hub checkpoint's names (transformers-5 load-time conversions), scales attached
+    try:
+        mapper = build_reverse_name_mapper(model)
+        state = revert_weight_conversion_quant_aware(model, state)
+        if mapper is not None:
+            revert_quant_config_names(hf_quant_config.get("quantization", {}), mapper)
+    except QuantConversionUnsupportedError as exc:
+        warnings.warn(f"Quant-aware reverse weight conversion skipped ({exc}); in-memory names kept.")
     gc = getattr(model, "generation_config", None)
     if gc is not None and (getattr(gc, "top_k", None) is not None or getattr(gc, "top_p", None) is not None):
         gc.do_sample = True
-    model.save_pretrained(export_dir, state_dict=state, max_shard_size=max_shard_size)
+    # transformers' own revert (which chokes on 0-d scales) must not run on the reverted dict
+    patches = []
+    for mod_path in ("transformers.core_model_loading", "transformers.modeling_utils"):
+        try:
+            mod = importlib.import_module(mod_path)
+        except ImportError:
+            continue
+        if hasattr(mod, "revert_weight_conversion"):
+            patches.append((mod, mod.revert_weight_conversion))
+            mod.revert_weight_conversion = lambda model, state_dict: state_dict
+    try:
+        model.save_pretrained(export_dir, state_dict=state, max_shard_size=max_shard_size)
+    finally:
+        for mod, orig in patches:
+            mod.revert_weight_conversion = orig
     q = hf_quant_config.get("quantization", {})
     quantization_config = None
     if q.get("quant_algo") is not None or q.get("kv_cache_quant_algo") is not None:

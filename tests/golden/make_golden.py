@@ -472,6 +472,21 @@ def export_cfg(name):
     return cfg
 
 
+def tiny_mixtral_export():
+    from transformers import MixtralConfig, MixtralForCausalLM
+
+    cfg = MixtralConfig(
+        hidden_size=64, intermediate_size=64, num_hidden_layers=2, num_attention_heads=4,
+        num_key_value_heads=2, vocab_size=32, max_position_embeddings=64, num_local_experts=4,
+        num_experts_per_tok=2, architectures=["MixtralForCausalLM"],
+    )
+    torch.manual_seed(82)
+    return MixtralForCausalLM(cfg).eval()
+
+
+EXPORT_MOE_CASES = {"moe_fp8": "FP8_DEFAULT_CFG", "moe_nvfp4": "NVFP4_DEFAULT_CFG"}
+
+
 def gen_export():
     """Unified HF checkpoint export (export/unified_export_hf.py export_hf_checkpoint) of a tiny
     Llama per format: the post-calibration state (weights + quantizer buffers) and the exported
@@ -485,9 +500,11 @@ def gen_export():
     g = torch.Generator().manual_seed(81)
     ids = torch.randint(0, 32, (4, 2, 16), generator=g)
     t, meta = {"calib_ids": ids}, {}
-    for name in EXPORT_CASES:
-        m = tiny_llama_export()
-        mtq.quantize(m, export_cfg(name), lambda mm: [mm(b) for b in ids])
+    for name in list(EXPORT_CASES) + list(EXPORT_MOE_CASES):
+        moe = name in EXPORT_MOE_CASES
+        m = tiny_mixtral_export() if moe else tiny_llama_export()
+        cfg = getattr(mtq, EXPORT_MOE_CASES[name]) if moe else export_cfg(name)
+        mtq.quantize(m, cfg, lambda mm: [mm(b) for b in ids])
         for k, v in m.state_dict().items():
             t[f"{name}.state.{k}"] = v.detach().clone().contiguous()
         with tempfile.TemporaryDirectory() as d:
@@ -499,7 +516,8 @@ def gen_export():
         hq["producer"]["version"] = None
         if cq and "producer" in cq:
             cq["producer"]["version"] = None
-        meta[name] = {"preset": EXPORT_CASES[name], "hf_quant_config": hq, "quantization_config": cq}
+        meta[name] = {"preset": (EXPORT_MOE_CASES if moe else EXPORT_CASES)[name], "model": "mixtral" if moe else "llama",
+                      "hf_quant_config": hq, "quantization_config": cq}
     save_file(t, str(OUT / "export.safetensors"))
     (OUT / "export.json").write_text(json.dumps(meta, indent=1))
 

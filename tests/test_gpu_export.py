@@ -31,6 +31,16 @@ def _tiny():
     return LlamaForCausalLM(cfg).eval()
 
 
+def _tiny_mixtral():
+    from transformers import MixtralConfig, MixtralForCausalLM
+
+    cfg = MixtralConfig(hidden_size=64, intermediate_size=64, num_hidden_layers=2, num_attention_heads=4,
+                        num_key_value_heads=2, vocab_size=32, max_position_embeddings=64, num_local_experts=4,
+                        num_experts_per_tok=2, architectures=["MixtralForCausalLM"])
+    torch.manual_seed(82)
+    return MixtralForCausalLM(cfg).eval()
+
+
 def _cfg(mtq, preset):
     cfg = copy.deepcopy(getattr(mtq, preset))
     for e in cfg["quant_cfg"]:
@@ -49,7 +59,7 @@ def test_export_matches_reference(gpu, case, tmp_path):
 
     t = load_file(str(G / "export.safetensors"))
     ids = t["calib_ids"].to(gpu)
-    model = _tiny().to(gpu)
+    model = (_tiny_mixtral() if META[case].get("model") == "mixtral" else _tiny()).to(gpu)
     mtq.quantize(model, _cfg(mtq, META[case]["preset"]), lambda m: [m(b) for b in ids])
     state = {k[len(case) + 7:]: v for k, v in t.items() if k.startswith(case + ".state.")}
     missing, unexpected = model.load_state_dict(state, strict=False)
