@@ -513,3 +513,55 @@ def cpu_threads() -> int:
 
 
 __all__ = [name for name in dir() if not name.startswith("_") and name not in ("math", "np", "torch")]
+
+
+# ----------------------------------------------------------------------------------------------
+# Checkpoint-export packing: restates export/quant_utils.py:792-938 and qtensor quantize()
+# ----------------------------------------------------------------------------------------------
+
+
+def export_fp8(weight, scale):
+    """(weight / scale).to(float8_e4m3fn) as bytes (quant_utils.py:855-867 / :881-913)."""
+    return (weight / scale).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def export_int4(weight, scale):
+    """pack_int4_in_uint8 (quant_utils.py:792-833), 2-D."""
+    out_dim, in_dim = weight.shape
+    block = in_dim // scale.shape[-1]
+    q = (weight / scale[:, torch.arange(in_dim) // block]).round().clamp(-8, 7).to(torch.int8)
+    r = q.T.reshape(in_dim, out_dim // 2, 2)
+    packed = (r[..., 0] & 0x0F) | ((r[..., 1] & 0x0F) << 4)
+    return packed.T.contiguous().view(torch.uint8)
+
+
+_NV_BOUNDS = torch.tensor([0.25, 0.75, 1.25, 1.75, 2.5, 3.5, 5])
+
+
+def export_nvfp4(weight, block_scale, scale_2):
+    """NVFP4QTensor.quantize with given scales (qtensor/nvfp4_tensor.py:253-342)."""
+    shape = weight.shape
+    block = weight.numel() // block_scale.numel()
+    w = weight.reshape(*shape[:-1], -1, block)
+    scaled = (w / (block_scale.float().reshape(*shape[:-1], -1) * scale_2).unsqueeze(-1)).reshape(shape)
+    sign = (scaled < 0).to(torch.uint8)
+    a = scaled.abs()
+    ordv = torch.searchsorted(_NV_BOUNDS, a, out_int32=True).to(torch.uint8)
+    eq = torch.any(a.unsqueeze(-1) == _NV_BOUNDS[[1, 3, 5]], dim=-1).to(torch.uint8)
+    q = (sign << 3) + ordv + eq
+    return (q[..., 1::2] << 4) | q[..., 0::2]
+
+
+def export_mxfp4(weight, block=32):
+    """MXFP4QTensor.quantize (qtensor/mxfp4_tensor.py:38-81): (packed codes, E8M0 bytes)."""
+    shape = weight.shape
+    x = weight.reshape(-1, block)
+    amax = x.float().abs().max(dim=-1, keepdim=True).values
+    descale = amax / 6.0
+    e = torch.ceil(torch.maximum(torch.log2(descale), torch.tensor(-127.0)))
+    q = (x / torch.exp2(e)).reshape(shape)
+    sign_bit = (2 - torch.sign(q)) // 2
+    ordv = torch.sum((q.abs().unsqueeze(-1) - _NV_BOUNDS) > 0, dim=-1)
+    codes = (sign_bit * 8 + ordv).to(torch.uint8)
+    packed = (codes[..., 1::2] << 4) + codes[..., 0::2]
+    return packed, (e + 127).to(torch.uint8)

@@ -1235,6 +1235,156 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_kernel(const T *__restr
   }
 }
 
+
+// ---- vectorised export packing (one 16 B input vector per lane, chunked non-temporal) --------
+template <int NB> struct ByteVec;
+template <> struct ByteVec<2> { using type = uint16_t; };
+template <> struct ByteVec<4> { using type = uint32_t; };
+template <> struct ByteVec<8> { using type = uint2; };
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__restrict__ x,
+                                                                   uint8_t *__restrict__ y,
+                                                                   int64_t nvec, int64_t cols,
+                                                                   const float *__restrict__ scale,
+                                                                   int per_row, int round_dtype) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  const float s = scale[per_row ? (i * N) / cols : 0];
+  const float r = 1.0f / s;
+  uint32_t b[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float q = div_rn(Elem<T>::ld(v.e[j]), s, r);
+    if (round_dtype) q = Elem<T>::ld(Elem<T>::st(q));
+    b[j] = e4m3_byte(q);
+  }
+  if constexpr (N == 8) {
+    uint2 o;
+    o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    o.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+    *reinterpret_cast<uint2 *>(y + i * N) = o;
+  } else {
+    *reinterpret_cast<uint32_t *>(y + i * N) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+  }
+}
+
+// rows (2p, 2p+1) x N columns -> N bytes
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__restrict__ x,
+                                                                    uint8_t *__restrict__ y,
+                                                                    int64_t nvec, int64_t cols,
+                                                                    const float *__restrict__ scale,
+                                                                    int64_t nblk, int block) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;  // over (rows/2) * cols / N
+  if (i >= nvec) return;
+  const int64_t cv = cols / N;
+  const int64_t pr = i / cv, c0 = (i - pr * cv) * N;
+  V lo = ldg_vec_nt(x + (2 * pr) * cols + c0);
+  V hi = ldg_vec_nt(x + (2 * pr + 1) * cols + c0);
+  const float s0 = scale[(2 * pr) * nblk + c0 / block], s1 = scale[(2 * pr + 1) * nblk + c0 / block];
+  const float r0 = 1.0f / s0, r1 = 1.0f / s1;
+  uint32_t b[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float q0 = __builtin_rintf(div_rn(Elem<T>::ld(lo.e[j]), s0, r0));
+    float q1 = __builtin_rintf(div_rn(Elem<T>::ld(hi.e[j]), s1, r1));
+    q0 = q0 < -8.f ? -8.f : (q0 > 7.f ? 7.f : q0);
+    q1 = q1 < -8.f ? -8.f : (q1 > 7.f ? 7.f : q1);
+    const int v0 = q0 != q0 ? 0 : (int)q0, v1 = q1 != q1 ? 0 : (int)q1;
+    b[j] = ((uint32_t)v0 & 0xFu) | (((uint32_t)v1 & 0xFu) << 4);
+  }
+  if constexpr (N == 8) {
+    uint2 o;
+    o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    o.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+    *reinterpret_cast<uint2 *>(y + pr * cols + c0) = o;
+  } else {
+    *reinterpret_cast<uint32_t *>(y + pr * cols + c0) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+  }
+}
+
+// one 16 B vector (N elements of one block) -> N/2 bytes
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__restrict__ x,
+                                                                     uint8_t *__restrict__ y,
+                                                                     int64_t nvec, int block,
+                                                                     const float *__restrict__ sblk,
+                                                                     const float *__restrict__ s2) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  const float d = sblk[(i * N) / block] * (*s2);
+  const float r = 1.0f / d;
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < N; j += 2) {
+    const uint32_t lo = nvfp4_code(div_rn(Elem<T>::ld(v.e[j]), d, r));
+    const uint32_t hi = nvfp4_code(div_rn(Elem<T>::ld(v.e[j + 1]), d, r));
+    o |= (lo | (hi << 4)) << (4 * j);
+  }
+  if constexpr (N == 8)
+    *reinterpret_cast<uint32_t *>(y + i * (N / 2)) = o;
+  else
+    *reinterpret_cast<uint16_t *>(y + i * (N / 2)) = (uint16_t)o;
+}
+
+// MXFP4: LPB = block / N lanes per block, shuffle-max, every lane writes N/2 code bytes, the
+// block's first lane its E8M0 byte.
+template <typename T, int BLOCK>
+__global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__restrict__ x,
+                                                                     uint8_t *__restrict__ y,
+                                                                     uint8_t *__restrict__ sc,
+                                                                     int64_t nvec) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  constexpr int LPB = BLOCK / N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i - (threadIdx.x % LPB) >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float a = fabsf(Elem<T>::ld(v.e[j]));
+    amax = (a > amax || a != a) ? a : amax;
+  }
+#pragma unroll
+  for (int o = LPB / 2; o > 0; o >>= 1) {
+    const float t = __shfl_xor(amax, o, 64);
+    amax = (t > amax || t != t) ? t : amax;
+  }
+  const float descale = amax / 6.0f;
+  float e;
+  if (descale != descale) {
+    e = descale;
+  } else {
+    const float l2 = descale > 0.f ? (float)log2((double)descale) : -INFINITY;
+    e = __builtin_ceilf(l2 > -127.f ? l2 : -127.f);
+  }
+  if (threadIdx.x % LPB == 0) sc[i / LPB] = (uint8_t)(int)(e + 127.f);
+  const float p = (e == e) ? exp2f(e) : e;
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float q = Elem<T>::ld(v.e[j]) / p;
+    const float a = fabsf(q);
+    const uint32_t ord = (a > 0.25f) + (a > 0.75f) + (a > 1.25f) + (a > 1.75f) + (a > 2.5f) +
+                         (a > 3.5f) + (a > 5.0f);
+    o |= (((q > 0.f) ? 0u : 8u) + ord) << (4 * j);
+  }
+  if constexpr (N == 8)
+    *reinterpret_cast<uint32_t *>(y + i * (N / 2)) = o;
+  else
+    *reinterpret_cast<uint16_t *>(y + i * (N / 2)) = (uint16_t)o;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1507,8 +1657,15 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
     const int64_t n = rows * cols;
-    export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
-        reinterpret_cast<const T *>(x), y, n, cols, scale, per_row, round_to_dtype);
+    constexpr int N = Vec<T>::N;
+    if (cols % N == 0 && aligned16(x) && ((uintptr_t)y % N) == 0) {
+      const int64_t nvec = n / N;
+      export_fp8_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, nvec, cols, scale, per_row, round_to_dtype);
+    } else {
+      export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, n, cols, scale, per_row, round_to_dtype);
+    }
     return check_launch();
   });
 }
@@ -1521,8 +1678,15 @@ int mtq_export_int4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int d
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
     const int64_t n = rows / 2 * cols;
-    export_int4_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
-        reinterpret_cast<const T *>(x), y, rows / 2, cols, scale, cols / block, block);
+    constexpr int N = Vec<T>::N;
+    if (cols % N == 0 && block % N == 0 && aligned16(x) && ((uintptr_t)y % N) == 0) {
+      const int64_t nvec = n / N;
+      export_int4_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, nvec, cols, scale, cols / block, block);
+    } else {
+      export_int4_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, rows / 2, cols, scale, cols / block, block);
+    }
     return check_launch();
   });
 }
@@ -1536,8 +1700,15 @@ int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int 
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
     const int64_t npairs = rows * cols / 2;
-    export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
-        reinterpret_cast<const T *>(x), y, npairs, cols, block_scale, scale_2, block);
+    constexpr int N = Vec<T>::N;
+    if (block % N == 0 && aligned16(x) && ((uintptr_t)y % (N / 2)) == 0) {
+      const int64_t nvec = rows * cols / N;
+      export_nvfp4_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, nvec, block, block_scale, scale_2);
+    } else {
+      export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, npairs, cols, block_scale, scale_2, block);
+    }
     return check_launch();
   });
 }
@@ -1550,8 +1721,18 @@ int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int 
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
     const int64_t nb = n / block;
-    export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(
-        reinterpret_cast<const T *>(x), y, scales, nb, block);
+    constexpr int N = Vec<T>::N;
+    if (aligned16(x) && ((uintptr_t)y % (N / 2)) == 0 && (block == 32 || block == 16) && block % N == 0) {
+      const int64_t nvec = n / N;
+      const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
+      if (block == 32)
+        export_mxfp4_vec_kernel<T, 32><<<g, kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+      else
+        export_mxfp4_vec_kernel<T, 16><<<g, kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+    } else {
+      export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, scales, nb, block);
+    }
     return check_launch();
   });
 }

@@ -500,3 +500,59 @@ def test_nvfp4_static_quantizer(gpu, dtype):
     out = q(lin.weight)
     ref = R.static_blockwise_fp4_fake_quant(w.reshape(-1, 16), amax, amax.amax()).reshape(w.shape)
     assert same_bits(out, ref), mismatch(out, ref)
+
+
+# --------------------------------------------------------------------------------------------
+# checkpoint export packing
+# --------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(96, 256), (10, 24), (7, 13)])
+def test_export_fp8_vs_oracle(gpu, dtype, shape):
+    g = torch.Generator().manual_seed(shape[0])
+    w = (torch.randn(shape, generator=g) * 0.05).to(dtype)
+    w.view(-1)[:4] = torch.tensor([0.0, -0.0, 10.0, -10.0]).to(dtype)  # 10 / s overflows -> NaN
+    s = w.float().abs().amax() / 448
+    ref = R.export_fp8(w, s)
+    out = ops().export_fp8(w.to(gpu), s.to(gpu), False, True).view(torch.uint8).cpu()
+    assert torch.equal(out, ref)
+    srow = w.float().abs().amax(dim=1) / 448
+    ref2 = R.export_fp8(w, srow[:, None])
+    out2 = ops().export_fp8(w.to(gpu), srow.to(gpu), True, False).view(torch.uint8).cpu()
+    assert torch.equal(out2, ref2)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape,block", [((64, 256), 128), ((6, 40), 8), ((4, 12), 4)])
+def test_export_int4_vs_oracle(gpu, dtype, shape, block):
+    g = torch.Generator().manual_seed(block)
+    w = (torch.randn(shape, generator=g) * 0.05).to(dtype)
+    s = w.float().reshape(shape[0], -1, block).abs().amax(-1) / 7
+    ref = R.export_int4(w, s)
+    out = ops().export_int4(w.to(gpu), s.to(gpu)).cpu()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(64, 256), (5, 48), (3, 2, 32)])
+def test_export_nvfp4_vs_oracle(gpu, dtype, shape):
+    g = torch.Generator().manual_seed(sum(shape))
+    w = (torch.randn(shape, generator=g) * 0.05).to(dtype)
+    s2 = w.float().abs().amax() / 2688
+    bs = (w.float().reshape(*shape[:-1], -1, 16).abs().amax(-1) / (6 * s2)).clamp(2**-9, 448)
+    bs = bs.to(torch.float8_e4m3fn).float()
+    ref = R.export_nvfp4(w, bs, s2)
+    out = ops().export_nvfp4(w.to(gpu), bs.to(gpu), s2.to(gpu)).cpu()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(64, 256), (3, 96)])
+def test_export_mxfp4_vs_oracle(gpu, dtype, shape):
+    g = torch.Generator().manual_seed(shape[1])
+    w = (torch.randn(shape, generator=g) * torch.logspace(-3, 1, shape[1])).to(dtype)
+    w[0, :32] = 0  # an all-zero block: exponent clamps at -127, zeros carry the sign bit
+    ref_q, ref_s = R.export_mxfp4(w, 32)
+    q, s = ops().export_mxfp4(w.to(gpu), 32)
+    assert torch.equal(q.cpu(), ref_q) and torch.equal(s.cpu().reshape(-1), ref_s.reshape(-1))
