@@ -1192,6 +1192,26 @@ __global__ __launch_bounds__(kThreads) void export_nvfp4_kernel(const T *__restr
   }
 }
 
+// ceil(max(log2(d), -127)) with log2 correctly rounded to fp32 (what torch.log2 gives): exact from
+// the exponent bits unless the significand is within 2^-10 of a power of two, where the rounding
+// of log2 can land on the integer -- only then is a double log2 taken.
+__device__ __forceinline__ float mx_e8m0_exponent(float d) {
+  if (d != d) return d;
+  if (!(d > 0.f)) return -127.f;
+  const uint32_t b = __float_as_uint(d);
+  const int ex = (int)((b >> 23) & 0xff) - 127;
+  const uint32_t m = b & 0x7fffffu;
+  float e;
+  if (((b >> 23) & 0xff) != 0 && m == 0) {
+    e = (float)ex;
+  } else if (((b >> 23) & 0xff) != 0 && m > (1u << 13)) {
+    e = (float)(ex + 1);
+  } else {
+    e = __builtin_ceilf((float)log2((double)d));
+  }
+  return e > -127.f ? e : -127.f;
+}
+
 // MXFP4QTensor.quantize (qtensor/mxfp4_tensor.py:38-81): per block of `block` along the flat
 // tensor, e = ceil(max(log2(amax / 6), -127)) (log2 correctly rounded to fp32), q = w / 2^e,
 // code = #(bounds < |q|) (ties toward zero) + 8 * (sign(q) <= 0) -- zero encodes with the sign bit
@@ -1209,14 +1229,7 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_kernel(const T *__restr
       const float a = fabsf(Elem<T>::ld(xb[k]));
       amax = (a > amax || a != a) ? a : amax;  // torch.max propagates NaN
     }
-    const float descale = amax / 6.0f;
-    float e;
-    if (descale != descale) {
-      e = descale;
-    } else {
-      const float l2 = descale > 0.f ? (float)log2((double)descale) : -INFINITY;
-      e = __builtin_ceilf(l2 > -127.f ? l2 : -127.f);
-    }
+    const float e = mx_e8m0_exponent(amax / 6.0f);
     sc[b] = (uint8_t)(int)(e + 127.f);
     const float p = (e == e) ? exp2f(e) : e;
     for (int k = 0; k < block; k += 2) {
@@ -1360,20 +1373,13 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
     const float t = __shfl_xor(amax, o, 64);
     amax = (t > amax || t != t) ? t : amax;
   }
-  const float descale = amax / 6.0f;
-  float e;
-  if (descale != descale) {
-    e = descale;
-  } else {
-    const float l2 = descale > 0.f ? (float)log2((double)descale) : -INFINITY;
-    e = __builtin_ceilf(l2 > -127.f ? l2 : -127.f);
-  }
+  const float e = mx_e8m0_exponent(amax / 6.0f);
   if (threadIdx.x % LPB == 0) sc[i / LPB] = (uint8_t)(int)(e + 127.f);
-  const float p = (e == e) ? exp2f(e) : e;
+  const float pinv = (e == e) ? exp2f(-e) : e;  // exact power of two: x * 2^-e == x / 2^e
   uint32_t o = 0;
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const float q = Elem<T>::ld(v.e[j]) / p;
+    const float q = Elem<T>::ld(v.e[j]) * pinv;
     const float a = fabsf(q);
     const uint32_t ord = (a > 0.25f) + (a > 0.75f) + (a > 1.25f) + (a > 1.75f) + (a > 2.5f) +
                          (a > 3.5f) + (a > 5.0f);
