@@ -48,8 +48,14 @@ def _dist_init(n_gpus: int):
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         local = int(os.environ.get("LOCAL_RANK", 0))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # MTQ_AMD_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU
+        backend = os.environ.get("MTQ_AMD_DIST_BACKEND", "nccl")
+        dev = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
         return dist, dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     return None, 0, 1
@@ -63,7 +69,8 @@ def _barrier(dist):
 def _max_over_ranks(dist, v: float) -> float:
     if dist is None:
         return v
-    t = torch.tensor([v], device="cuda", dtype=torch.float64)
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
