@@ -208,6 +208,39 @@ int mtq_mse_accumulate(const void *a, const void *b, int64_t n, int dtype, float
 int mtq_mul_cols(const void *x, const void *scale, void *y, int64_t rows, int64_t cols, int dtype,
                  hipStream_t stream);
 
+/* ---- calibration searches (csrc/mtq_search.hip) ---------------------------------------------
+ *  mtq_nvfp4_fp8_scale_sweep: NVFP4MSECalibrator's fused FP8-scale sweep
+ *    (kernels/quantization/gemm/nvfp4_fp8_sweep.py:62-160 `nvfp4_fp8_scale_sweep`, called from
+ *    calib/mse.py:267-287): x [n_blocks, block] (block 8/16/32), per block the candidate c of
+ *    `candidates` (the 126 E4M3 values / 448) minimising sum(|w| - e2m1(|w|/s)*s)^2 with
+ *    s = RN(RN(c*g)/6); best_amax[b] = RN(g * c_best) (fp32), g = *global_amax.
+ *  mtq_mse_sweep: MseCalibrator.collect (calib/mse.py:82-125) of one tensor with every candidate
+ *    at once: x [rows, cols] (the calibrator's fp32 view; any float dtype, read exactly),
+ *    amax [rows] (amax_per_row) or [1]; candidate amax = amax * c, rounded to amax_dtype when
+ *    round_candidate_amax (torch promotion of a dimensioned amax), quantised as the INT-n
+ *    (num_bits >= 1) or E4M3 (num_bits == 0) fake-quant kernels do;
+ *    loss[k, r] = sum_c (x - xq)^2.  Rows longer than 128 need a workspace of
+ *    mtq_mse_sweep_workspace_floats(rows, cols, n_candidates) floats (no zero-fill needed).
+ *  mtq_awq_clip_search: the block branch of awq_clip's `_clip_search` (model_calib.py:1815-1882)
+ *    for static-block INT-n weights: w [co, cols] (zero-padded to a multiple of block),
+ *    x [n_tokens, cols] fp32 (the stride-sampled, padded activations), w_amax [co * cols/block];
+ *    for clip ratio i and block (o, b):
+ *      loss[i, o, b] (+)= mean_t float(T(dot_T(x_t, qdq(w, T(amax*shrink_i))) - dot_T(x_t, w)))^2
+ *    where dot_T rounds every product and the sum to T (the reference's (inputs * w).sum(-1)). */
+int mtq_nvfp4_fp8_scale_sweep(const void *x, float *best_amax, int64_t n_blocks, int block,
+                              int dtype, const float *global_amax, const float *candidates,
+                              int n_candidates, hipStream_t stream);
+int64_t mtq_mse_sweep_workspace_floats(int64_t rows, int64_t cols, int n_candidates);
+int mtq_mse_sweep(const void *x, int64_t rows, int64_t cols, int dtype, const void *amax,
+                  int amax_dtype, int amax_per_row, int round_candidate_amax,
+                  const float *candidates, int n_candidates, int num_bits, int is_unsigned,
+                  int narrow_range, float *loss, float *workspace, int64_t workspace_floats,
+                  hipStream_t stream);
+int mtq_awq_clip_search(const void *w, const float *x, int64_t co, int64_t cols, int64_t n_tokens,
+                        int dtype, const void *w_amax, int amax_dtype, const float *shrinks,
+                        int n_shrinks, int block, int num_bits, int is_unsigned, int narrow_range,
+                        float *loss, int accumulate, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -565,3 +565,123 @@ def export_mxfp4(weight, block=32):
     codes = (sign_bit * 8 + ordv).to(torch.uint8)
     packed = (codes[..., 1::2] << 4) + codes[..., 0::2]
     return packed, (e + 127).to(torch.uint8)
+
+
+# ----------------------------------------------------------------------------------------------
+# MSE weight calibration: calib/mse.py:31-300, model_calib.py:639-827,
+# kernels/quantization/gemm/{_fp8_scale_candidates.py:25-32, nvfp4_fp8_sweep.py:62-160}
+# ----------------------------------------------------------------------------------------------
+
+
+def fp8_scale_candidates():
+    """The 126 finite positive E4M3 values / 448 (_fp8_scale_candidates.py:25-32), fp32."""
+    u = torch.arange(0, 128, dtype=torch.uint8).view(torch.float8_e4m3fn).float()
+    return u[torch.isfinite(u) & (u > 0)] / 448.0
+
+
+def _fp4_round_magnitude(a):
+    """common/nvfp4_quant.py:31-62: nearest E2M1 magnitude by the reference's threshold chain."""
+    return np.where(a <= 0.25, 0.0, np.where(a < 0.75, 0.5, np.where(a <= 1.25, 1.0, np.where(
+        a < 1.75, 1.5, np.where(a <= 2.5, 2.0, np.where(a < 3.5, 3.0, np.where(a <= 5.0, 4.0, 6.0))))))).astype(np.float32)
+
+
+def nvfp4_fp8_scale_sweep(x, global_amax, block_size=16):
+    """Per-block best amax of the fused FP8-scale sweep (nvfp4_fp8_sweep.py:62-105): for each of the
+    126 candidates c, ``scale = RN(RN(c*g)/6)`` (1 when 0), ``loss = sum((|w| - e2m1(|w|/scale)*scale)^2)``
+    in fp32 with the row sum in the 8-way pairwise order of numpy (= the Triton interpreter's
+    tl.sum, which the golden vectors come from), strict ``<`` so the first minimum wins, and
+    ``best = RN(g * c[best])``."""
+    w = np.abs(x.detach().float().reshape(-1, block_size).numpy())
+    g = np.float32(float(global_amax))
+    cands = fp8_scale_candidates().numpy()
+    best_loss = np.full(w.shape[0], np.inf, dtype=np.float32)
+    best_idx = np.zeros(w.shape[0], dtype=np.int64)
+    for k, c in enumerate(cands):
+        scale = np.float32(np.float32(c * g) / np.float32(6.0))
+        safe = np.float32(1.0) if scale == 0 else scale
+        qm = _fp4_round_magnitude((w / safe).astype(np.float32))
+        diff = (w - (qm * safe).astype(np.float32)).astype(np.float32)
+        loss = np.sum(diff * diff, axis=1, dtype=np.float32)
+        better = loss < best_loss
+        best_loss = np.where(better, loss, best_loss)
+        best_idx = np.where(better, k, best_idx)
+    return torch.from_numpy((g * cands[best_idx]).astype(np.float32))
+
+
+def mse_candidates(step_size=0.1, start_multiplier=0.25, stop_multiplier=4.0):
+    """MseCalibrator._generate_candidates (calib/mse.py:58-80)."""
+    n = math.ceil((stop_multiplier - start_multiplier) / step_size) + 1
+    return torch.linspace(start_multiplier, stop_multiplier, steps=n)
+
+
+def mse_sweep(x, initial_amax, quant_fn, axis, candidates=None):
+    """MseCalibrator.collect + compute_amax (calib/mse.py:82-183) for one tensor: per candidate
+    ``xq = quant_fn(x, initial_amax * c)``, ``loss = sum((x - xq)^2)`` over the non-axis dims, then
+    the first argmin per channel.  Returns (losses [K, ...], best amax)."""
+    x = x.detach().float()
+    cands = mse_candidates() if candidates is None else candidates
+    red = convert_quantization_axis_to_reduce_axis(x, axis)
+    losses = []
+    for c in cands:
+        xq = quant_fn(x, initial_amax * c)
+        err = torch.nn.functional.mse_loss(x, xq, reduction="none")
+        losses.append(torch.sum(err) if red is None else torch.sum(err, dim=red))
+    losses = torch.stack(losses)
+    best = cands[torch.argmin(losses, dim=0)]
+    if best.ndim != 0:
+        best = best.view_as(initial_amax)
+    return losses, initial_amax * best
+
+
+# ----------------------------------------------------------------------------------------------
+# AWQ-clip block search: model_calib.py:1725-1940 (_clip_search :1800-1882, update_best_params
+# :1785-1797)
+# ----------------------------------------------------------------------------------------------
+
+
+def awq_clip_shrinks(min_clip_ratio=0.5, shrink_step=0.05):
+    """model_calib.py:1757-1759."""
+    return [round(float(k), 2) for k in torch.arange(min_clip_ratio, 1.0, shrink_step)] + [1.0]
+
+
+def awq_clip_block_losses(weight, inputs, w_amax, shrinks, block, num_bits=4, unsigned=False,
+                          narrow_range=False, co_bsz=1024, max_tokens=64):
+    """One `_clip_search` call (model_calib.py:1815-1882) for a static-block INT-n weight: returns
+    ({shrink: loss [co_batch rows, n_block]} stacked as [S, co, n_block], tokens used).  The ATen
+    op sequence is the reference's: stride-sampled tokens, zero padding to the block, the
+    dtype-rounded ``(inputs * w).sum(-1)`` per block, ``(cur - org).float().pow(2).mean(1)``."""
+    co, ci = weight.shape
+    x = inputs.reshape(-1, inputs.shape[-1])
+    x = x[0 :: max(1, x.shape[0] // max_tokens)]
+    ntok = x.shape[0]
+    w = weight
+    if ci % block:
+        w = torch.nn.functional.pad(w, (0, block - ci % block), "constant", 0)
+        x = torch.nn.functional.pad(x, (0, block - ci % block), "constant", 0)
+    cip = w.shape[-1]
+    w4 = w.reshape(co, 1, -1, block)
+    x4 = x.reshape(1, ntok, -1, block)
+    out = torch.zeros(len(shrinks), co, cip // block)
+    for s_i, shrink in enumerate(shrinks):
+        amax = w_amax * shrink
+        # the weight quantizer's static block path: blocks of the (padded) weight, per-block amax
+        wq = tensor_quant(w.reshape(-1, block), amax.reshape(-1, 1), num_bits, unsigned, narrow_range)
+        wq = wq.reshape(co, 1, -1, block)
+        for b0 in range(0, co, co_bsz):
+            sl = slice(b0, min(b0 + co_bsz, co))
+            org = (x4 * w4[sl]).sum(dim=-1)
+            cur = (x4 * wq[sl]).sum(dim=-1)
+            out[s_i, sl] = (cur - org).float().pow(2).mean(dim=1)
+    return out, ntok
+
+
+def awq_clip_best(losses, w_amax, shrinks):
+    """update_best_params (model_calib.py:1785-1797): first strictly-smaller loss wins."""
+    best_loss = torch.ones_like(w_amax) * float("inf")
+    best = torch.zeros_like(w_amax)
+    for s_i, shrink in enumerate(shrinks):
+        loss = losses[s_i].reshape(w_amax.shape)
+        idx = loss < best_loss
+        best_loss = torch.where(idx, loss, best_loss)
+        best = torch.where(idx, w_amax * shrink, best)
+    return best

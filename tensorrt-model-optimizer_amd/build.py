@@ -53,7 +53,8 @@ def _run(cmd: list[str]) -> None:
 
 def build_kernels(force: bool = False) -> Path:
     out = OUT / "libmtq_amd.so"
-    deps = [CSRC / "mtq_kernels.hip", CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
+    srcs = [CSRC / "mtq_kernels.hip", CSRC / "mtq_search.hip"]
+    deps = srcs + [CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
     if force or _stale(out, deps):
         OUT.mkdir(parents=True, exist_ok=True)
         tmp = out.with_suffix(".so.tmp")
@@ -68,7 +69,7 @@ def build_kernels(force: bool = False) -> Path:
                 "-Wall",
                 "-Wno-unused-function",
                 f"-I{INC}",
-                str(CSRC / "mtq_kernels.hip"),
+                *[str(p) for p in srcs],
                 "-o",
                 str(tmp),
             ]

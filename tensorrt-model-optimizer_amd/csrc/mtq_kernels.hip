@@ -1393,6 +1393,12 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
 
 }  // namespace
 
+// shared with the other translation units of libmtq_amd.so (mtq_search.hip)
+namespace mtq {
+int host_check_launch() { return check_launch(); }
+int host_num_cus() { return num_cus(); }
+}  // namespace mtq
+
 // ============================================================================================
 // C ABI
 // ============================================================================================

@@ -452,6 +452,88 @@ std::tuple<at::Tensor, at::Tensor> export_mxfp4(const at::Tensor &weight, int64_
   return {y, sc};
 }
 
+// ---- calibration searches (mtq_search.hip) ------------------------------------------------
+// nvfp4_fp8_scale_sweep(x [n_blocks, block], global_amax, candidates [126] fp32) -> best amax
+// [n_blocks] fp32 (kernels/quantization/gemm/nvfp4_fp8_sweep.py:108-160).
+at::Tensor nvfp4_fp8_scale_sweep(const at::Tensor &inputs, const at::Tensor &global_amax,
+                                 const at::Tensor &candidates, int64_t block_size) {
+  check_device(inputs, "x");
+  TORCH_CHECK_VALUE(block_size > 0 && inputs.numel() % block_size == 0, "x.numel() (",
+                    inputs.numel(), ") is not divisible by block_size (", block_size, ").");
+  at::Tensor x = inputs.contiguous();
+  const int dt = checked_dtype(x, "x");
+  TORCH_CHECK(dt != MTQ_F64, "nvfp4_fp8_scale_sweep: float64 is not supported");
+  at::Tensor g = global_amax.to(x.device(), at::kFloat).reshape({1}).contiguous();
+  at::Tensor c = candidates.to(x.device(), at::kFloat).contiguous();
+  const int64_t nb = x.numel() / block_size;
+  at::Tensor best = at::empty({nb}, x.options().dtype(at::kFloat));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_nvfp4_fp8_scale_sweep(x.data_ptr(), best.data_ptr<float>(), nb, (int)block_size,
+                                         dt, g.data_ptr<float>(), c.data_ptr<float>(),
+                                         (int)c.numel(), cur_stream(x)),
+               "nvfp4_fp8_scale_sweep");
+  return best;
+}
+
+// mse_sweep(x [rows, cols], amax [rows] or [1], candidates [K], num_bits (0 = e4m3), unsigned,
+// narrow_range, round_candidate_amax) -> loss [K, rows] fp32 (calib/mse.py:82-125).
+at::Tensor mse_sweep(const at::Tensor &inputs, const at::Tensor &amax, const at::Tensor &candidates,
+                     int64_t num_bits, bool is_unsigned, bool narrow_range,
+                     bool round_candidate_amax) {
+  check_device(inputs, "x");
+  TORCH_CHECK(inputs.dim() == 2, "mse_sweep: x must be 2-D [rows, cols]");
+  at::Tensor x = inputs.contiguous();
+  const int dt = checked_dtype(x, "x");
+  TORCH_CHECK(dt != MTQ_F64, "mse_sweep: float64 is not supported");
+  const int64_t rows = x.size(0), cols = x.size(1);
+  at::Tensor a = amax.to(x.device()).contiguous();
+  const int adt = checked_dtype(a, "amax");
+  TORCH_CHECK(a.numel() == 1 || a.numel() == rows, "mse_sweep: amax must have 1 or rows elements");
+  at::Tensor c = candidates.to(x.device(), at::kFloat).contiguous();
+  const int k = (int)c.numel();
+  at::Tensor loss = at::empty({k, rows}, x.options().dtype(at::kFloat));
+  const int64_t wsn = mtq_mse_sweep_workspace_floats(rows, cols, k);
+  TORCH_CHECK(wsn >= 0, "mse_sweep: invalid shape");
+  at::Tensor ws = at::empty({std::max<int64_t>(wsn, 1)}, x.options().dtype(at::kFloat));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_mse_sweep(x.data_ptr(), rows, cols, dt, a.data_ptr(), adt,
+                             a.numel() != 1 || rows == 1 ? 1 : 0, round_candidate_amax ? 1 : 0,
+                             c.data_ptr<float>(), k, (int)num_bits, is_unsigned, narrow_range,
+                             loss.data_ptr<float>(), ws.data_ptr<float>(), wsn, cur_stream(x)),
+               "mse_sweep");
+  return loss;
+}
+
+// awq_clip_search(w [co, cols], x [tokens, cols] fp32, w_amax [co * cols/block], shrinks [S],
+// loss [S, co, cols/block] fp32 (in/out), block, num_bits, unsigned, narrow_range, accumulate)
+// (model_calib.py:1815-1882).
+void awq_clip_search(const at::Tensor &weight, const at::Tensor &x, const at::Tensor &w_amax,
+                     const at::Tensor &shrinks, at::Tensor loss, int64_t block, int64_t num_bits,
+                     bool is_unsigned, bool narrow_range, bool accumulate) {
+  check_device(weight, "weight");
+  TORCH_CHECK(weight.dim() == 2 && x.dim() == 2 && x.size(1) == weight.size(1),
+              "awq_clip_search: weight [co, cols] and x [tokens, cols] expected");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous(), "awq_clip_search: x must be fp32 contiguous");
+  at::Tensor w = weight.contiguous();
+  const int dt = checked_dtype(w, "weight");
+  TORCH_CHECK(dt != MTQ_F64, "awq_clip_search: float64 is not supported");
+  at::Tensor a = w_amax.contiguous();
+  const int adt = checked_dtype(a, "w_amax");
+  const int64_t co = w.size(0), cols = w.size(1);
+  TORCH_CHECK(block > 0 && cols % block == 0, "awq_clip_search: cols must be a multiple of block");
+  TORCH_CHECK(a.numel() == co * (cols / block), "awq_clip_search: w_amax must have co*cols/block elements");
+  at::Tensor s = shrinks.to(w.device(), at::kFloat).contiguous();
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.is_contiguous() &&
+                  loss.numel() == s.numel() * co * (cols / block),
+              "awq_clip_search: loss must be fp32 contiguous [S, co, cols/block]");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
+  check_status(mtq_awq_clip_search(w.data_ptr(), x.data_ptr<float>(), co, cols, x.size(0), dt,
+                                   a.data_ptr(), adt, s.data_ptr<float>(), (int)s.numel(), (int)block,
+                                   (int)num_bits, is_unsigned, narrow_range, loss.data_ptr<float>(),
+                                   accumulate ? 1 : 0, cur_stream(w)),
+               "awq_clip_search");
+}
+
 at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at::Tensor> &pqs,
                                int64_t block, int64_t num_bits, bool is_unsigned,
                                bool narrow_range) {
@@ -581,6 +663,11 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("export_int4(Tensor weight, Tensor scale) -> Tensor");
   m.def("export_nvfp4(Tensor weight, Tensor block_scale, Tensor scale_2) -> Tensor");
   m.def("export_mxfp4(Tensor weight, int block) -> (Tensor, Tensor)");
+  m.def("nvfp4_fp8_scale_sweep(Tensor x, Tensor global_amax, Tensor candidates, int block_size=16) -> Tensor");
+  m.def("mse_sweep(Tensor x, Tensor amax, Tensor candidates, int num_bits, bool unsigned, "
+        "bool narrow_range, bool round_candidate_amax) -> Tensor");
+  m.def("awq_clip_search(Tensor weight, Tensor x, Tensor w_amax, Tensor shrinks, Tensor(a!) loss, "
+        "int block, int num_bits, bool unsigned, bool narrow_range, bool accumulate) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
@@ -604,6 +691,9 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("export_int4", &export_int4);
   m.impl("export_nvfp4", &export_nvfp4);
   m.impl("export_mxfp4", &export_mxfp4);
+  m.impl("nvfp4_fp8_scale_sweep", &nvfp4_fp8_scale_sweep);
+  m.impl("mse_sweep", &mse_sweep);
+  m.impl("awq_clip_search", &awq_clip_search);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {

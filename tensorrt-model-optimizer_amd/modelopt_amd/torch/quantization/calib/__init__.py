@@ -3,5 +3,6 @@
 from .calibrator import _Calibrator
 from .histogram import HistogramCalibrator
 from .max import MaxCalibrator
+from .mse import MseCalibrator, NVFP4MSECalibrator
 
-__all__ = ["HistogramCalibrator", "MaxCalibrator", "_Calibrator"]
+__all__ = ["HistogramCalibrator", "MaxCalibrator", "MseCalibrator", "NVFP4MSECalibrator", "_Calibrator"]

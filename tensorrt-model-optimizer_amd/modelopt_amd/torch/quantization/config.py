@@ -342,6 +342,18 @@ class MaxCalibConfig(QuantizeAlgorithmConfig):
     shared_states: Any = None
 
 
+class MseCalibConfig(QuantizeAlgorithmConfig):
+    """``mse`` weight-amax search (reference config.py:938-998)."""
+
+    method: str | None = "mse"
+    step_size: float | None = Field(default=0.1, gt=0.0)
+    start_multiplier: float | None = Field(default=0.25, gt=0.0)
+    stop_multiplier: float | None = Field(default=4.0, gt=0.0)
+    fp8_scale_sweep: bool | None = False
+    distributed_sync: bool | None = True
+    shared_states: Any = None
+
+
 class AWQLiteCalibConfig(QuantizeAlgorithmConfig):
     method: str | None = "awq_lite"
     alpha_step: float = Field(default=0.1, gt=0.0, le=1.0)
@@ -363,6 +375,7 @@ class AWQFullCalibConfig(AWQLiteCalibConfig, AWQClipCalibConfig):
 
 _ALGO_CONFIGS: dict[str, type[QuantizeAlgorithmConfig]] = {
     "max": MaxCalibConfig,
+    "mse": MseCalibConfig,
     "awq_lite": AWQLiteCalibConfig,
     "awq_clip": AWQClipCalibConfig,
     "awq_full": AWQFullCalibConfig,
@@ -382,7 +395,7 @@ def algorithm_config(algorithm) -> QuantizeAlgorithmConfig | None:
     if cls is None:
         raise NotImplementedError(
             f"modelopt_amd: calibration algorithm {method!r} is outside the MI355X-native hot path "
-            "(supported: max, awq_lite, awq_clip, awq_full)"
+            "(supported: max, mse, awq_lite, awq_clip, awq_full)"
         )
     return cls(**algorithm)
 
@@ -501,6 +514,12 @@ _NVFP4 = {"num_bits": (2, 1), "effective_bits": 4.5,
           "block_sizes": {-1: 16, "type": "dynamic", "scale_bits": (4, 3)}}
 NVFP4_DEFAULT_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, "max")
 NVFP4_AWQ_LITE_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, "awq_lite")
+NVFP4_AWQ_CLIP_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, {"method": "awq_clip"})
+NVFP4_AWQ_FULL_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, {"method": "awq_full", "alpha_step": 0.1})
+_NVFP4_STATIC = {"num_bits": (2, 1), "block_sizes": {-1: 16, "type": "static", "scale_bits": (4, 3)}}
+NVFP4_W4A4_WEIGHT_MSE_FP8_SWEEP_CFG: dict[str, Any] = _preset(
+    _NVFP4_STATIC, _NVFP4, {"method": "mse", "fp8_scale_sweep": True}
+)
 W4A8_AWQ_BETA_CFG: dict[str, Any] = _preset(
     [{"num_bits": 4, "block_sizes": {-1: 128, "type": "static"}}, {"num_bits": (4, 3), "axis": None}],
     {"num_bits": (4, 3), "axis": None},
@@ -538,6 +557,9 @@ __all__ += [
     "W4A8_MXFP4_FP8_CFG",
     "NVFP4_DEFAULT_CFG",
     "NVFP4_AWQ_LITE_CFG",
+    "NVFP4_AWQ_CLIP_CFG",
+    "NVFP4_AWQ_FULL_CFG",
+    "NVFP4_W4A4_WEIGHT_MSE_FP8_SWEEP_CFG",
     "W4A8_AWQ_BETA_CFG",
     "FP8_KV_CFG",
     "NVFP4_KV_CFG",

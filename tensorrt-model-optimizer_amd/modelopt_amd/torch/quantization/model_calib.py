@@ -506,16 +506,303 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
             delattr(module, "awq_lite")
 
 
+# ---- AWQ-clip (reference model_calib.py:1725-1940) -----------------------------------------------
+
+_CLIP_KERNEL_BLOCKS = (8, 16, 32, 64, 128)
+
+
+class _AWQClipHelper:
+    """Per-linear clip-search state (reference AWQClipHelper, :1746-1783).  The per-shrink losses
+    live in one [S, co, n_block] fp32 tensor; ``loss`` is the reference's {shrink: view} dict."""
+
+    def __init__(self, module, min_clip_ratio: float, shrink_step: float):
+        self.num_tokens = 0
+        self.block_size = _get_awq_quantizer_block_size(module.weight, module.weight_quantizer)
+        wq = module.weight_quantizer
+        wq.reset_amax()
+        enable_stats_collection(wq)
+        wq(module.weight)
+        finish_stats_collection(wq)
+        self.w_amax = wq.amax.clone()
+        co, ci = module.weight.shape
+        self.shrinks = [round(float(k), 2) for k in torch.arange(min_clip_ratio, 1.0, shrink_step)] + [1.0]
+        dev = module.weight.device
+        if self.is_per_tensor_clip(module):
+            self.loss_tensor = torch.zeros(len(self.shrinks), device=dev)
+        else:
+            self.loss_tensor = torch.zeros(len(self.shrinks), co, math.ceil(ci / self.block_size), device=dev)
+        self.loss = {k: self.loss_tensor[i] for i, k in enumerate(self.shrinks)}
+        self.best_clip_val = None
+        self.best_loss = None
+        self.is_input_quantized = module.input_quantizer.is_enabled
+        wq.disable()
+
+    @staticmethod
+    def is_per_tensor_clip(module) -> bool:
+        q = module.weight_quantizer
+        dyn = q.block_sizes is not None and q.block_sizes.get("type", None) == "dynamic" and q.axis is None
+        return dyn or (q.axis is None and q.block_sizes is None)
+
+
+def _awq_clip_update_best_params(module):
+    """reference :1785-1797: first strictly smaller loss wins, best = w_amax * shrink."""
+    h = module.awq_clip
+    h.best_loss = torch.ones_like(h.w_amax) * float("inf")
+    h.best_clip_val = torch.zeros_like(h.w_amax)
+    for shrink, loss in h.loss.items():
+        loss = loss.view_as(h.w_amax)
+        idx = loss < h.best_loss
+        h.best_loss = torch.where(idx, loss, h.best_loss)
+        h.best_clip_val = torch.where(idx, h.w_amax * shrink, h.best_clip_val)
+
+
+def _clip_kernel_ok(module, inputs) -> bool:
+    wq, w = module.weight_quantizer, module.weight
+    bs = module.awq_clip.block_size
+    return (
+        isinstance(wq, TensorQuantizer)
+        and type(wq).__name__ in ("TensorQuantizer", "StaticBlockScaleQuantizer")
+        and isinstance(wq._num_bits, int)
+        and wq.fake_quant
+        and wq.backend is None
+        and wq.pre_quant_scale is None
+        and wq.is_static_block_quant
+        and len([k for k in (wq.block_sizes or {}) if isinstance(k, int)]) == 1
+        and bs in _CLIP_KERNEL_BLOCKS
+        and w.dim() == 2
+        and w.is_cuda
+        and w.dtype in _FAST_DTYPES
+        and inputs.dtype == w.dtype
+        and len(module.awq_clip.shrinks) <= 63
+        and module.awq_clip.w_amax.numel() == w.shape[0] * math.ceil(w.shape[1] / bs)
+    )
+
+
+def _clip_search(self, inputs, co_bsz=256, max_tokens=16):
+    """One clip-search step on a forward (reference :1800-1882)."""
+    h = self.awq_clip
+    weight = self.weight
+    self.weight_quantizer.enable()
+    if h.is_per_tensor_clip(self):
+        # NVFP4 / per-tensor: only the per-tensor amax is clipped (reference :1804-1815)
+        out_actual = inputs @ weight.T
+        original_amax = self.weight_quantizer.amax.clone()
+        h.num_tokens += inputs.shape[0]
+        for i, shrink in enumerate(h.shrinks):
+            self.weight_quantizer.amax = original_amax * shrink
+            out = inputs @ self.weight_quantizer(weight).T
+            if _mse_fast(out, out_actual):
+                _ops().mse_accumulate(out, out_actual, h.loss_tensor, i)
+            else:
+                h.loss_tensor[i] += (out - out_actual).float().pow(2).mean()
+        return
+    x = inputs.reshape(-1, inputs.shape[-1])
+    x = x[0 :: max(1, x.shape[0] // max_tokens)]
+    h.num_tokens += x.shape[0]
+    bs = h.block_size
+    co, ci = weight.shape
+    group = self.parallel_state.data_parallel_group if self.parallel_state is not None else None
+    dp = group is not None and group.is_initialized()
+    if _clip_kernel_ok(self, x):
+        # one HIP pass per forward: every (row, block, clip ratio) of the weight at once
+        pad = (-ci) % bs
+        xs = x.float()
+        w = weight.detach()
+        if pad:
+            xs = F.pad(xs, (0, pad))
+            w = F.pad(w, (0, pad))
+        xs = xs.contiguous()
+        wq = self.weight_quantizer
+        shrinks = torch.tensor(h.shrinks, dtype=torch.float32)
+        if dp:
+            part = torch.empty_like(h.loss_tensor)
+            _ops().awq_clip_search(w, xs, h.w_amax, shrinks, part, bs, wq._num_bits, wq._unsigned, wq._narrow_range, False)
+            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group.group)
+            part /= group.world_size()
+            h.loss_tensor += part
+        else:
+            _ops().awq_clip_search(w, xs, h.w_amax, shrinks, h.loss_tensor, bs, wq._num_bits, wq._unsigned,
+                                   wq._narrow_range, True)
+        return
+    # the reference's op sequence (any other quantizer), on the device
+    if ci % bs != 0:
+        weight = F.pad(weight, (0, bs - ci % bs), "constant", 0)
+        x = F.pad(x, (0, bs - ci % bs), "constant", 0)
+    weight = weight.reshape(co, 1, -1, bs)
+    x = x.reshape(1, x.shape[0], -1, bs)
+    for b0 in range(0, co, co_bsz):
+        sl = slice(b0, min(b0 + co_bsz, co))
+        w = weight[sl]
+        org_out = (x * w).sum(dim=-1)
+        for i, shrink in enumerate(h.shrinks):
+            self.weight_quantizer.amax = h.w_amax * shrink
+            cur_w = self.weight_quantizer(self.weight)[sl]
+            if cur_w.shape[-1] % bs != 0:
+                cur_w = F.pad(cur_w, (0, bs - cur_w.shape[-1] % bs), "constant", 0)
+            cur_out = (x * cur_w.reshape(w.shape)).sum(dim=-1)
+            loss = (cur_out - org_out).float().pow(2).mean(dim=1)
+            if dp:
+                dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group.group)
+                loss /= group.world_size()
+            h.loss_tensor[i, sl] += loss
+
+
+def _awq_clip_forward(self, input, *args, **kwargs):
+    """Patched QuantLinear forward during AWQ-clip (reference :1884-1908)."""
+    h = self.awq_clip
+    if h.is_input_quantized:
+        self.input_quantizer.enable()
+        max_calibrate(self.input_quantizer, lambda iq: iq(input))
+        self.input_quantizer.disable()
+    if input.numel() > 0:
+        _clip_search(self, self.input_quantizer(input), h.max_co_batch_size, h.max_tokens_per_batch)
+    self.weight_quantizer.disable()
+    return self._forward_no_awq(input, *args, **kwargs)
+
+
+@torch.no_grad()
+def awq_clip(model: nn.Module, forward_loop: ForwardLoop, max_co_batch_size: int = 1024,
+             max_tokens_per_batch: int = 64, min_clip_ratio: float = 0.5, shrink_step: float = 0.05,
+             debug: bool = False, **kwargs):
+    """AWQ-clip: per-block clipped amax search on the calibration activations (reference
+    :1725-1940).  The block search of a static-block INT weight is one HIP pass per forward
+    (``torch.ops.modelopt_amd.awq_clip_search``)."""
+    assert forward_loop is not None, "forward_loop must be provided for awq_clip"
+    patched = []
+    for name, module in model.named_modules():
+        if (
+            is_quantized_linear(module)
+            and module.weight_quantizer.is_enabled
+            and module.weight_quantizer.block_sizes is not None
+        ):
+            module.awq_clip = _AWQClipHelper(module, min_clip_ratio, shrink_step)
+            module.awq_clip.max_co_batch_size = max_co_batch_size
+            module.awq_clip.max_tokens_per_batch = max_tokens_per_batch
+            module._forward_no_awq = module.forward
+            module.forward = _awq_clip_forward.__get__(module, type(module))
+            patched.append(module)
+    enable_stats_collection(model)
+    forward_loop(model)
+    with set_quantizer_by_cfg_context(model, [{"quantizer_name": "*weight_quantizer", "enable": False}]):
+        max_calibrate(model, lambda m: None, distributed_sync=True)
+    finish_stats_collection(model)
+    for module in patched:
+        h = module.awq_clip
+        if h.num_tokens > 0:
+            _awq_clip_update_best_params(module)
+            module.weight_quantizer.amax = h.best_clip_val
+            module.weight_quantizer.enable()
+            if h.is_input_quantized:
+                module.input_quantizer.enable()
+        if not debug:
+            delattr(module, "awq_clip")
+        for k in ("forward", "_forward_no_awq"):
+            if k in module.__dict__:
+                del module.__dict__[k]
+
+
 def awq(model: nn.Module, forward_loop: ForwardLoop | None = None, algorithm: str = "awq_lite", **kwargs):
-    """AWQ dispatch (reference :1362-1391); awq_clip is a 'next' item."""
+    """AWQ dispatch (reference :1362-1391): awq_lite, awq_clip, or both (awq_full)."""
     with SequentialQuantizer.convert_to_single_quantizer(model):
         if algorithm in ["awq_full", "awq_lite"]:
             awq_lite(model, forward_loop, **{k: v for k, v in kwargs.items() if k in ("alpha_step", "debug")})
         if algorithm in ["awq_full", "awq_clip"]:
-            raise NotImplementedError("modelopt_amd: awq_clip is a next-round item (SURVEY §8f rank 3)")
+            clip_keys = ("max_co_batch_size", "max_tokens_per_batch", "min_clip_ratio", "shrink_step", "debug")
+            awq_clip(model, forward_loop, **{k: v for k, v in kwargs.items() if k in clip_keys})
     for _, module in model.named_modules():
         if is_quantized_linear(module) and isinstance(module.weight_quantizer, SequentialQuantizer):
             max_calibrate(module, lambda lin: lin.weight_quantizer(lin.weight))
 
+
+
+# ---- MSE weight calibration (reference model_calib.py:639-827) ---------------------------------
+
+
+def _run_and_load_max_stats(model: nn.Module, forward_loop: ForwardLoop | None = None):
+    """Collect + load stats without post-processing (reference :202-209)."""
+    enable_stats_collection(model)
+    if forward_loop is None:
+        weight_only_quantize(model)
+    else:
+        forward_loop(model)
+    finish_stats_collection(model)
+
+
+def _mse_quant_func(x, amax, quantizer):
+    """Fake-quantise ``x`` (the calibrator's block layout) with a candidate ``amax`` (reference
+    :639-662): quant on, calib off, fake quant on, the original shape restored around the call."""
+    original_amax = quantizer._amax.clone() if hasattr(quantizer, "_amax") else None
+    quantizer._amax = amax
+    flags = (quantizer._if_quant, quantizer._if_calib, quantizer._fake_quant)
+    quantizer._if_quant, quantizer._if_calib, quantizer._fake_quant = True, False, True
+    try:
+        if hasattr(quantizer, "_original_shape"):
+            x = quantizer._reset_to_original_shape(x)
+        xq = quantizer(x)
+        if hasattr(quantizer, "_block_reshape_size"):
+            xq = quantizer._process_for_blockquant(xq)
+    finally:
+        quantizer._if_quant, quantizer._if_calib, quantizer._fake_quant = flags
+        if original_amax is not None:
+            quantizer._amax = original_amax
+        else:
+            delattr(quantizer, "_amax")
+    return xq
+
+
+def _make_weight_mse_calibrator(weight_quantizer, step_size, start_multiplier, stop_multiplier,
+                                fp8_scale_sweep, error_func=None, hessian=None):
+    """The MSE calibrator for one eligible weight quantizer, or None (reference :665-730)."""
+    from functools import partial
+
+    from .calib.mse import MseCalibrator, NVFP4MSECalibrator
+
+    if (
+        not isinstance(weight_quantizer, TensorQuantizer)
+        or not weight_quantizer.is_enabled
+        or weight_quantizer._dynamic
+        or weight_quantizer.is_mx_format
+        or weight_quantizer._calibrator is None
+        or getattr(weight_quantizer, "_amax", None) is None
+    ):
+        return None
+    initial_amax = weight_quantizer._amax.clone().detach()
+    axis = weight_quantizer._calibrator._axis
+    quant_func = partial(_mse_quant_func, quantizer=weight_quantizer)
+    if fp8_scale_sweep:
+        if weight_quantizer.backend is None and getattr(weight_quantizer, "is_nvfp4_static", False):
+            return NVFP4MSECalibrator(amax=initial_amax, axis=axis, global_amax=weight_quantizer.global_amax,
+                                      quant_func=quant_func, error_func=error_func, hessian=hessian)
+        return None  # fp8_scale_sweep: only static NVFP4 weights are swept
+    return MseCalibrator(amax=initial_amax, axis=axis, step_size=step_size, start_multiplier=start_multiplier,
+                         stop_multiplier=stop_multiplier, quant_func=quant_func, error_func=error_func)
+
+
+@torch.no_grad()
+def _mse_calibrate_weights(model, name_to_module, step_size, start_multiplier, stop_multiplier, fp8_scale_sweep):
+    """MSE-refine every eligible weight quantizer in place (reference :779-826)."""
+    seen = set()
+    for parent in name_to_module.values():
+        if id(parent) in seen or not isinstance(parent, QuantModule):
+            continue
+        seen.add(id(parent))
+        for weight, weight_quantizer in parent.iter_weights_for_calibration():
+            cal = _make_weight_mse_calibrator(weight_quantizer, step_size, start_multiplier, stop_multiplier,
+                                              fp8_scale_sweep)
+            if cal is None:
+                continue
+            weight_quantizer._calibrator = cal
+            _run_and_load_max_stats(weight_quantizer, lambda q, w=weight: q(w))
+            if hasattr(cal, "reset"):
+                cal.reset()
+
+
+def mse_calibrate(model: nn.Module, forward_loop: ForwardLoop | None = None, distributed_sync=True,
+                  step_size: float = 0.1, start_multiplier: float = 0.25, stop_multiplier: float = 4.0,
+                  fp8_scale_sweep: bool = False, shared_states=None):
+    """Max calibration, then an MSE search of every weight amax (reference :733-776)."""
+    max_calibrate(model, forward_loop, distributed_sync, shared_states=shared_states)
+    _mse_calibrate_weights(model, dict(model.named_modules()), step_size, start_multiplier, stop_multiplier,
+                           fp8_scale_sweep)
 
 _ = math

@@ -21,7 +21,7 @@ import torch.nn as nn
 from .config import QuantizeConfig, algorithm_config
 from .conversion import convert_to_quantized_model, quantizer_state, set_quantizer_attributes_partial
 from .layerwise import layerwise_calibrate
-from .model_calib import awq, max_calibrate
+from .model_calib import awq, max_calibrate, mse_calibrate
 from .nn.modules.quant_module import QuantModule
 from .nn.modules.tensor_quantizer import SequentialQuantizer, TensorQuantizer
 from .utils.names import is_quantized
@@ -49,6 +49,8 @@ def _apply_algorithm(model, algo_cfg, forward_loop):
     if method == "max":
         kwargs.pop("shared_states", None)
         func = max_calibrate
+    elif method == "mse":
+        func = mse_calibrate
     elif method in ("awq_lite", "awq_full", "awq_clip"):
         kwargs["algorithm"] = method
         func = awq

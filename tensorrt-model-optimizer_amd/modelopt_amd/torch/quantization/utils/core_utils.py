@@ -22,6 +22,7 @@ __all__ = [
     "convert_quantization_axis_to_reduce_axis",
     "reduce_amax",
     "reduce_amax_accumulate",
+    "reduce_sum",
 ]
 
 
@@ -122,3 +123,12 @@ def reduce_amax(input, axis=None, keepdims=True, squeeze_scalar=True):
     if squeeze_scalar and out.numel() == 1:
         out.squeeze_()
     return out
+
+
+def reduce_sum(input, axis=None, keepdims=True):
+    """Sum over ``axis`` (all dims when None) -- reference core_utils.py:187-212."""
+    if axis is None:
+        return torch.sum(input)
+    if isinstance(axis, int):
+        axis = (axis,)
+    return torch.sum(input, dim=axis, keepdim=keepdims)

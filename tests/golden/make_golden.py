@@ -522,13 +522,180 @@ def gen_export():
     (OUT / "export.json").write_text(json.dumps(meta, indent=1))
 
 
+def gen_mse():
+    """MSE weight calibration (calib/mse.py, model_calib.py:733-827).
+
+    * ``sweep.*``: the reference's fused NVFP4 FP8-scale sweep Triton kernel
+      (kernels/quantization/gemm/nvfp4_fp8_sweep.py ``_fp8_scale_sweep_kernel``) run on CPU via the
+      Triton interpreter (fp32 arithmetic only -- none of the interpreter's cast quirks apply), on
+      ``[n_blocks, block]`` weights (the wrapper's CUDA check is bypassed by calling the kernel).
+    * ``cal.*``: ``MseCalibrator`` multiplier search with the reference TensorQuantizer as
+      quant_func (per-tensor FP8, per-channel INT8, static-block INT4), incl. every candidate's loss.
+    * ``model.*``: ``mtq.quantize(tiny Llama, {"method": "mse"})`` weight amaxes for INT8 / FP8.
+    """
+    import copy
+    from functools import partial
+
+    import triton
+
+    from modelopt.torch.kernels.quantization.gemm import _fp8_scale_candidates as cand_mod
+    from modelopt.torch.kernels.quantization.gemm import nvfp4_fp8_sweep as sweep_mod
+    from modelopt.torch.quantization.calib import MseCalibrator
+    from modelopt.torch.quantization.model_calib import _mse_quant_func
+
+    t, meta = {}, {"sweep": {}, "cal": {}, "model": {}}
+    g = torch.Generator().manual_seed(90)
+    kern = sweep_mod._fp8_scale_sweep_kernel.fn  # the JIT function under the autotuner
+    cases = [("f32_b16", torch.float32, 512, 16), ("bf16_b16", torch.bfloat16, 640, 16),
+             ("f16_b16", torch.float16, 256, 16), ("f32_b32", torch.float32, 128, 32),
+             ("bf16_b8", torch.bfloat16, 256, 8), ("f32_zero", torch.float32, 16, 16)]
+    for name, dt, nb, bs in cases:
+        x = (torch.randn(nb, bs, generator=g) * torch.logspace(-3, 1, nb)[:, None]).to(dt)
+        if name == "f32_zero":
+            x.zero_()
+        elif name.startswith("bf16_b16"):
+            x[3] = 0
+            x[5, :] = x[5, 0]  # all-equal magnitudes
+        ga = x.float().abs().amax()
+        cands = cand_mod.fp8_scale_candidates("cpu").float()
+        best = torch.empty(nb, dtype=torch.float32)
+        kern[(triton.cdiv(nb, 16),)](x.contiguous().view(-1), cands, ga.reshape(1), best, nb,
+                                     BLOCK_SIZE=bs, NUM_CANDIDATES=int(cands.numel()),
+                                     BLOCKS_PER_PROGRAM=16)
+        t[f"sweep.{name}.x"], t[f"sweep.{name}.global_amax"], t[f"sweep.{name}.best"] = x, ga.reshape(()), best
+        meta["sweep"][name] = {"blocks": nb, "block": bs}
+    t["sweep.candidates"] = cand_mod.fp8_scale_candidates("cpu").float()
+
+    # MseCalibrator with the reference quantizer as quant_func
+    qcases = [("fp8_tensor", {"num_bits": (4, 3), "axis": None}, torch.float32, (64, 128)),
+              ("int8_ch", {"num_bits": 8, "axis": 0}, torch.float32, (48, 96)),
+              ("int8_ch_bf16", {"num_bits": 8, "axis": 0}, torch.bfloat16, (32, 128)),
+              ("int4_blk", {"num_bits": 4, "block_sizes": {-1: 32, "type": "static"}}, torch.float32, (16, 128)),
+              ("fp8_tensor_bf16", {"num_bits": (4, 3), "axis": None}, torch.bfloat16, (64, 64))]
+    for name, qc, dt, shape in qcases:
+        w = (torch.randn(shape, generator=g) * torch.logspace(-1, 0.5, shape[0])[:, None]).to(dt)
+        w[0, 0] = 8.0  # an outlier for the clipping trade-off
+        q = TensorQuantizer(QuantizerAttributeConfig(**qc))
+        q.enable_calib(); q.disable_quant()
+        q(w)
+        q.load_calib_amax()
+        q.disable_calib(); q.enable_quant()
+        init = q._amax.clone()
+        cal = MseCalibrator(amax=init, axis=q._calibrator._axis, quant_func=partial(_mse_quant_func, quantizer=q))
+        q._calibrator = cal
+        q.enable_calib(); q.disable_quant()
+        q(w)
+        losses = torch.stack([ls.reshape(-1) for ls in cal._losses_sum])
+        best = cal.compute_amax()
+        t[f"cal.{name}.w"], t[f"cal.{name}.init_amax"] = w, init
+        t[f"cal.{name}.losses"], t[f"cal.{name}.best"] = losses, best.clone()
+        t[f"cal.{name}.candidates"] = cal._candidates.clone()
+        meta["cal"][name] = {"cfg": {k: (list(v) if isinstance(v, tuple) else v) for k, v in qc.items() if k != "block_sizes"},
+                             "block": (qc.get("block_sizes") or {}).get(-1), "dtype": str(dt), "axis": q._calibrator._axis}
+
+    # end to end: mtq.quantize with {"method": "mse"}
+    g2 = torch.Generator().manual_seed(91)
+    ids = torch.randint(0, 32, (2, 2, 16), generator=g2)
+    t["model.calib_ids"] = ids
+    for name, preset in [("int8", "INT8_DEFAULT_CFG"), ("fp8", "FP8_DEFAULT_CFG")]:
+        m = tiny_llama()
+        cfg = copy.deepcopy(getattr(mtq, preset))
+        cfg["algorithm"] = {"method": "mse"}
+        mtq.quantize(m, cfg, lambda mm: [mm(b) for b in ids])
+        for n, mod in m.named_modules():
+            if isinstance(mod, TensorQuantizer) and mod.is_enabled and getattr(mod, "_amax", None) is not None:
+                t[f"model.{name}.{n}"] = mod._amax.clone()
+        meta["model"][name] = preset
+    save_file(t, str(OUT / "mse.safetensors"))
+    (OUT / "mse.json").write_text(json.dumps(meta, indent=1))
+
+
+class _ClipMLP(nn.Module):
+    """The reference AWQ tests' toy model shape (test_calib.py:38-56): bias-free 16 -> f1 -> f2 -> 16."""
+
+    def __init__(self, f1=32, f2=16):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(16, f1, bias=False), nn.ReLU(), nn.Linear(f1, f2, bias=False),
+                                 nn.ReLU(), nn.Linear(f2, 16, bias=False))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def gen_awq_clip():
+    """AWQ-clip / AWQ-full (model_calib.py:1725-1940) on the reference test's _SimpleMLP (INT4,
+    block 8; test_calib.py:125-283), a padded variant (ci not a multiple of the block) and a bf16
+    linear with block 128 (the products and sums rounded to bf16 as the reference's
+    ``(inputs * w).sum(-1)``), with debug=True so every per-shrink loss is recorded."""
+    import copy
+
+    def awq_cfg(method, block):
+        cfg = copy.deepcopy(mtq.INT4_AWQ_CFG)
+        for e in cfg["quant_cfg"]:
+            if e.get("quantizer_name") == "*weight_quantizer":
+                e["cfg"]["block_sizes"] = {-1: block, "type": "static"}
+        cfg["algorithm"] = {"method": method, "debug": True}
+        if method != "awq_clip":
+            cfg["algorithm"]["alpha_step"] = 0.1
+        return cfg
+
+    t, meta = {}, {}
+    g = torch.Generator().manual_seed(95)
+
+    def record(name, model, data, test):
+        t[f"{name}.test"] = test
+        for n, mod in model.named_modules():
+            if hasattr(mod, "awq_clip"):
+                h = mod.awq_clip
+                t[f"{name}.{n}.w_amax"] = h.w_amax.clone()
+                t[f"{name}.{n}.best_clip"] = h.best_clip_val.clone()
+                t[f"{name}.{n}.losses"] = torch.stack([v.reshape(-1) for v in h.loss.values()])
+                t[f"{name}.{n}.amax"] = mod.weight_quantizer.amax.clone()
+                t[f"{name}.{n}.weight"] = mod.weight.detach().clone()
+                if mod.input_quantizer.pre_quant_scale is not None:
+                    t[f"{name}.{n}.pqs"] = mod.input_quantizer.pre_quant_scale.clone()
+                meta[name]["layers"][n] = {"shrinks": [float(k) for k in h.loss], "num_tokens": int(h.num_tokens)}
+        with torch.no_grad():
+            t[f"{name}.out"] = model(test.clone()).detach()
+
+    for name, method, f1, f2, block in [("mlp_clip", "awq_clip", 32, 16, 8), ("mlp_full", "awq_full", 32, 16, 8),
+                                        ("mlp_full_pad", "awq_full", 13, 19, 8)]:
+        torch.manual_seed(96)
+        model = _ClipMLP(f1=f1, f2=f2)
+        t[f"{name}.sd"] = torch.cat([v.reshape(-1) for v in model.state_dict().values()])
+        for k, v in model.state_dict().items():
+            t[f"{name}.sd.{k}"] = v.clone()
+        data = [torch.randn(2, 64, 16, generator=g) for _ in range(2)]
+        for i, d in enumerate(data):
+            t[f"{name}.data{i}"] = d
+        meta[name] = {"method": method, "block": block, "f1": f1, "f2": f2, "layers": {}}
+        mtq.quantize(model, awq_cfg(method, block), lambda mm: [mm(d.clone()) for d in data])
+        record(name, model, data, torch.randn(3, 16, generator=g))
+
+    # bf16 linear, block 128, 3 batches of 4 x 80 tokens (stride-sampled to 64 per batch)
+    name = "bf16_lin"
+    torch.manual_seed(97)
+    lin = nn.Sequential(nn.Linear(384, 192, bias=False)).to(torch.bfloat16)
+    for k, v in lin.state_dict().items():
+        t[f"{name}.sd.{k}"] = v.clone()
+    data = [torch.randn(4, 80, 384, generator=g).to(torch.bfloat16) for _ in range(3)]
+    for i, d in enumerate(data):
+        t[f"{name}.data{i}"] = d
+    meta[name] = {"method": "awq_clip", "block": 128, "layers": {}}
+    mtq.quantize(lin, awq_cfg("awq_clip", 128), lambda mm: [mm(d) for d in data])
+    record(name, lin, data, torch.randn(2, 384, generator=g).to(torch.bfloat16))
+    save_file(t, str(OUT / "awq_clip.safetensors"))
+    (OUT / "awq_clip.json").write_text(json.dumps(meta, indent=1))
+
+
 def gen_presets():
     names = [
         "INT8_DEFAULT_CFG", "INT8_WEIGHT_ONLY_CFG", "FP8_DEFAULT_CFG", "FP8_PER_CHANNEL_PER_TOKEN_CFG",
         "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG", "INT4_BLOCKWISE_WEIGHT_ONLY_CFG", "INT4_AWQ_CFG",
         "MXFP8_DEFAULT_CFG", "MXFP6_DEFAULT_CFG", "MXFP4_DEFAULT_CFG", "MXINT8_DEFAULT_CFG",
         "W4A8_MXFP4_FP8_CFG", "MXFP4_MLP_WEIGHT_ONLY_CFG", "NVFP4_DEFAULT_CFG", "NVFP4_AWQ_LITE_CFG",
-        "W4A8_AWQ_BETA_CFG", "FP8_KV_CFG", "NVFP4_KV_CFG",
+        "W4A8_AWQ_BETA_CFG", "FP8_KV_CFG", "NVFP4_KV_CFG", "NVFP4_AWQ_CLIP_CFG", "NVFP4_AWQ_FULL_CFG",
+        "NVFP4_W4A4_WEIGHT_MSE_FP8_SWEEP_CFG",
     ]
 
     def enc(o):
@@ -575,7 +742,7 @@ def gen_mx_kat():
 
 
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "export", "awq", "presets", "mx_kat"]
+    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "export", "awq", "mse", "awq_clip", "presets", "mx_kat"]
     for s in steps:
         print("generating", s, flush=True)
         globals()["gen_" + s]()

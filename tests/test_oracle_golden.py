@@ -159,3 +159,80 @@ def test_nvfp4_static_scales_match_reference():
         assert torch.equal(R.compute_fp4_scales(amax, amax.amax()), t[f"{name}.scale"])
         assert torch.equal(R.compute_fp4_scales(amax, amax.amax() * 2), t[f"{name}.scale_g2"])
         assert torch.equal(R.compute_fp4_scales(amax, None, True, 256.0), t[f"{name}.scale_46"])
+
+
+# ---- MSE weight calibration (calib/mse.py) and AWQ-clip (model_calib.py:1725-1940) ----------
+
+
+@pytest.fixture(scope="module")
+def mse_gold():
+    return load_file(str(G / "mse.safetensors")), json.loads((G / "mse.json").read_text())
+
+
+def test_nvfp4_sweep_oracle_matches_reference_triton_kernel(mse_gold):
+    t, meta = mse_gold
+    assert torch.equal(R.fp8_scale_candidates(), t["sweep.candidates"])
+    for name, m in meta["sweep"].items():
+        got = R.nvfp4_fp8_scale_sweep(t[f"sweep.{name}.x"], t[f"sweep.{name}.global_amax"], m["block"])
+        assert bits_equal(got, t[f"sweep.{name}.best"]), name
+
+
+def _mse_quant_fn(name, m):
+    if m["cfg"]["num_bits"] == [4, 3]:
+        return lambda x, a: R.fp8_eager(x, a)
+    nb = m["cfg"]["num_bits"]
+    return lambda x, a: R.tensor_quant(x, a, nb, False, False)
+
+
+def test_mse_sweep_oracle_matches_reference(mse_gold):
+    t, meta = mse_gold
+    for name, m in meta["cal"].items():
+        w = t[f"cal.{name}.w"].float()
+        if m["block"]:
+            w = w.reshape(-1, m["block"])
+        axis = tuple(m["axis"]) if isinstance(m["axis"], list) else m["axis"]
+        losses, best = R.mse_sweep(w, t[f"cal.{name}.init_amax"], _mse_quant_fn(name, m), axis)
+        assert torch.equal(losses.reshape(losses.shape[0], -1), t[f"cal.{name}.losses"]), name
+        assert bits_equal(best, t[f"cal.{name}.best"]), name
+
+
+@pytest.fixture(scope="module")
+def clip_gold():
+    return load_file(str(G / "awq_clip.safetensors")), json.loads((G / "awq_clip.json").read_text())
+
+
+def _layer_inputs(t, name, layers, data_keys):
+    """The activations each linear sees in the reference forward (pre_quant_scale applied)."""
+    acts = {n: [] for n in layers}
+    for dk in data_keys:
+        x = t[dk]
+        for n in layers:
+            pqs = t.get(f"{name}.{n}.pqs")
+            xin = x * pqs if pqs is not None else x
+            acts[n].append(xin)
+            x = torch.nn.functional.linear(xin, t[f"{name}.{n}.weight"])
+            if n != layers[-1]:
+                x = torch.relu(x)
+    return acts
+
+
+def test_awq_clip_oracle_matches_reference(clip_gold):
+    t, meta = clip_gold
+    for name, m in meta.items():
+        layers = list(m["layers"])
+        data_keys = sorted(k for k in t if k.startswith(f"{name}.data"))
+        acts = _layer_inputs(t, name, layers, data_keys)
+        for n in layers:
+            shrinks = m["layers"][n]["shrinks"]
+            assert shrinks == R.awq_clip_shrinks()
+            w, w_amax = t[f"{name}.{n}.weight"], t[f"{name}.{n}.w_amax"]
+            total, ntok = None, 0
+            for x in acts[n]:
+                loss, k = R.awq_clip_block_losses(w, x, w_amax, shrinks, m["block"])
+                total = loss if total is None else total + loss
+                ntok += k
+            assert ntok == m["layers"][n]["num_tokens"], (name, n)
+            assert torch.equal(total.reshape(len(shrinks), -1), t[f"{name}.{n}.losses"]), (name, n)
+            best = R.awq_clip_best(total, w_amax, shrinks)
+            assert bits_equal(best, t[f"{name}.{n}.best_clip"]), (name, n)
+            assert bits_equal(t[f"{name}.{n}.amax"].reshape(best.shape), best), (name, n)
