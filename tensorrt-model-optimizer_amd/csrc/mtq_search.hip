@@ -286,6 +286,21 @@ __global__ __launch_bounds__(kThreads) void mse_finish_kernel(const float *__res
   loss[(int64_t)k * rows + r] = acc;
 }
 
+// Many chunks per row (per-tensor MSE): a workgroup per (row, candidate); lane t sums chunks
+// t, t + 256, ... in order, then a fixed-shape tree -- deterministic for a given shape.
+__global__ __launch_bounds__(kThreads) void mse_finish_wide_kernel(const float *__restrict__ partials,
+                                                                    int64_t rows, int64_t nchunk,
+                                                                    int ncand,
+                                                                    float *__restrict__ loss) {
+  __shared__ float red[kThreads / 64];
+  const int64_t r = blockIdx.x / ncand;
+  const int k = (int)(blockIdx.x - r * ncand);
+  float acc = 0.f;
+  for (int64_t c = threadIdx.x; c < nchunk; c += kThreads) acc += partials[(r * nchunk + c) * ncand + k];
+  const float tot = block_sum(acc, red);
+  if (threadIdx.x == 0) loss[(int64_t)k * rows + r] = tot;
+}
+
 // ============================================================================================
 // AWQ-clip block search (model_calib.py:1815-1882, static-block INT-n weights)
 // ============================================================================================
@@ -491,8 +506,12 @@ int mtq_mse_sweep(const void *x, int64_t rows, int64_t cols, int dtype, const vo
     int st = host_check_launch();
     if (st != MTQ_OK) return st;
     const int64_t n = rows * n_candidates;
-    mse_finish_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-        workspace, rows, nchunk, n_candidates, loss);
+    if (nchunk > 64)
+      mse_finish_wide_kernel<<<(unsigned)n, kThreads, 0, stream>>>(workspace, rows, nchunk,
+                                                                    n_candidates, loss);
+    else
+      mse_finish_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+          workspace, rows, nchunk, n_candidates, loss);
     return host_check_launch();
   });
 }
