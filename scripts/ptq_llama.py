@@ -76,7 +76,7 @@ def build_model(layers: int, device, model="llama3-8b"):
 
 
 def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", rank=0, world=1, baseline=True,
-        model_name="llama3-8b", algorithm=None):
+        model_name="llama3-8b", algorithm=None, kv=None):
     import modelopt_amd.torch.quantization as mtq
 
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -108,12 +108,16 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     cfg = getattr(mtq, config)
-    if algorithm is not None:
+    if algorithm is not None or kv is not None:
         import copy
 
         cfg = copy.deepcopy(cfg)
+    if algorithm is not None:
         cfg["algorithm"] = algorithm
         res["algorithm"] = algorithm
+    if kv is not None:  # e.g. FP8_KV_CFG: K/V cache fake quant inside every attention
+        cfg["quant_cfg"] = cfg["quant_cfg"] + getattr(mtq, kv)["quant_cfg"]
+        res["kv"] = kv
     mtq.quantize(model, cfg, forward_loop)
     torch.cuda.synchronize()
     res["ptq_wall_clock_s"] = round(time.perf_counter() - t0, 3)
@@ -141,8 +145,9 @@ if __name__ == "__main__":
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--config", default="FP8_DEFAULT_CFG")
     ap.add_argument("--no-baseline", action="store_true")
+    ap.add_argument("--kv", default=None, help="KV preset appended to the config, e.g. FP8_KV_CFG")
     ap.add_argument("--algorithm", default=None, help='JSON override, e.g. \'{"method": "awq_full"}\'')
     a = ap.parse_args()
     algo = json.loads(a.algorithm) if a.algorithm else None
     print(json.dumps(run(a.samples, a.seq, a.batch, a.layers, a.config, baseline=not a.no_baseline,
-                         model_name=a.model, algorithm=algo)), flush=True)
+                         model_name=a.model, algorithm=algo, kv=a.kv)), flush=True)

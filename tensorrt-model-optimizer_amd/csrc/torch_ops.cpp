@@ -189,8 +189,15 @@ at::Tensor fake_tensor_quant_with_axis(const at::Tensor &inputs, const at::Tenso
 
 // ---- FP8 -----------------------------------------------------------------------------------
 at::Tensor fp8_qdq(const at::Tensor &inputs, const at::Tensor &amax_in);
+// Per-tensor element-wise qdq is layout-free: a dense, non-overlapping strided input (e.g. the
+// transposed [B, H, S, D] K/V states of HF attention) is processed in its storage order and the
+// output gets the same strides (empty_like preserves them), instead of a .contiguous() copy.
+bool storage_order_ok(const at::Tensor &t, const at::Tensor &amax) {
+  return amax.numel() == 1 && !t.is_contiguous() && t.is_non_overlapping_and_dense();
+}
+
 at::Tensor fp8_qdq(const at::Tensor &inputs, const at::Tensor &amax_in) {
-  at::Tensor x = inputs.contiguous();
+  at::Tensor x = storage_order_ok(inputs, amax_in) ? inputs : inputs.contiguous();
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
   at::Tensor amax = amax_operand(amax_in, x);
@@ -576,7 +583,7 @@ at::Tensor quantize_op(const at::Tensor &input, const at::Tensor &amax, int64_t 
   if (num_bits == 8 && exponent_bits == 4) return fp8_qdq(input, amax);
   TORCH_CHECK_VALUE(exponent_bits == 0, "Invalid combination of (num_bits, exponent_bits): (",
                     num_bits, ", ", exponent_bits, ").");
-  at::Tensor x = input.contiguous();
+  at::Tensor x = storage_order_ok(input, amax) ? input : input.contiguous();
   at::Tensor y = at::empty_like(x);
   int_qdq_into(x, y, amax, num_bits, is_unsigned, narrow_range);
   return y;

@@ -642,7 +642,7 @@ def postprocess_state_dict(state_dict: dict, maxbound: float, kv_cache_format: s
                     assert kv_cache_format in (KV_CACHE_FP8, KV_CACHE_NVFP4, KV_CACHE_NVFP4_AFFINE), (
                         "Invalid KV cache quantization format."
                     )
-                    value = value.float() / maxbound
+                    value = _div(value.float(), maxbound)  # true division (CPU reference rounding)
                 out[prefix + new] = value
                 break
     # squeeze (1, n, m) scales

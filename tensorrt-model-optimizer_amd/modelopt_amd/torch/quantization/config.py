@@ -531,6 +531,35 @@ FP8_KV_CFG: dict[str, Any] = {
 NVFP4_KV_CFG: dict[str, Any] = {
     "quant_cfg": [{"quantizer_name": "*[kv]_bmm_quantizer", "cfg": copy.deepcopy(_NVFP4)}],
 }
+_AFFINE = {"bias": {-2: None, -4: None, "type": "static"}}
+FP8_AFFINE_KV_CFG: dict[str, Any] = {
+    "quant_cfg": [
+        {"quantizer_name": "*[kv]_bmm_quantizer", "cfg": {"num_bits": (4, 3), "axis": None}},
+        {"quantizer_name": "*[kv]_bmm_quantizer", "cfg": {"num_bits": (4, 3), "axis": None, **copy.deepcopy(_AFFINE)}},
+    ],
+}
+NVFP4_AFFINE_KV_CFG: dict[str, Any] = {
+    "quant_cfg": [
+        {"quantizer_name": "*[kv]_bmm_quantizer", "cfg": copy.deepcopy(_NVFP4)},
+        {"quantizer_name": "*[kv]_bmm_quantizer", "cfg": {**copy.deepcopy(_NVFP4), **copy.deepcopy(_AFFINE)}},
+    ],
+}
+_FP8_PT = {"num_bits": (4, 3), "axis": None}
+NVFP4_FP8_MHA_CONFIG: dict[str, Any] = {
+    "quant_cfg": copy.deepcopy(
+        _BASE_DISABLE_ALL
+        + [
+            {"quantizer_name": "*weight_quantizer", "cfg": _NVFP4},
+            {"quantizer_name": "*input_quantizer", "cfg": _NVFP4},
+            {"quantizer_name": "*output_quantizer", "enable": False},
+            {"quantizer_name": "*[qkv]_bmm_quantizer", "cfg": _FP8_PT},
+            {"quantizer_name": "*softmax_quantizer", "cfg": _FP8_PT},
+            {"quantizer_name": "*p_bmm_quantizer", "cfg": _FP8_PT},
+            {"quantizer_name": "transformer_blocks*bmm2_output_quantizer", "cfg": _FP8_PT},
+        ]
+    ),
+    "algorithm": "max",
+}
 MXFP4_MLP_WEIGHT_ONLY_CFG: dict[str, Any] = {
     "quant_cfg": _BASE_DISABLE_ALL
     + [
@@ -563,6 +592,9 @@ __all__ += [
     "W4A8_AWQ_BETA_CFG",
     "FP8_KV_CFG",
     "NVFP4_KV_CFG",
+    "FP8_AFFINE_KV_CFG",
+    "NVFP4_AFFINE_KV_CFG",
+    "NVFP4_FP8_MHA_CONFIG",
 ]
 
 ForwardLoop = Callable[[Any], Any]

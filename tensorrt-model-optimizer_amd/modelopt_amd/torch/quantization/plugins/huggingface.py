@@ -11,6 +11,8 @@ with that structure (reference :1697-1720), so ``mtq.quantize`` on a Mixtral mod
 from __future__ import annotations
 
 import contextlib
+import functools
+import inspect
 
 import torch
 import torch.nn as nn
@@ -19,7 +21,13 @@ from ..nn.modules.quant_module import QuantModule, QuantModuleRegistry
 from ..nn.modules.tensor_quantizer import TensorQuantizer
 from . import register_on_the_fly
 
-__all__ = ["_QuantFusedExperts", "force_eager_experts_impl_on_the_fly", "register_fused_experts_on_the_fly"]
+__all__ = [
+    "_QuantAttention",
+    "_QuantFusedExperts",
+    "force_eager_experts_impl_on_the_fly",
+    "register_fused_experts_on_the_fly",
+    "register_hf_attentions_on_the_fly",
+]
 
 
 @contextlib.contextmanager
@@ -146,6 +154,109 @@ def force_eager_experts_impl_on_the_fly(model):
                 _force(getattr(cfg, sub))
 
     _force(getattr(model, "config", None))
+
+
+class _QuantAttention(QuantModule):
+    """KV-cache / attention-BMM quantization for transformers attention modules that dispatch
+    through ``ALL_ATTENTION_FUNCTIONS`` (reference plugins/huggingface.py:78-410).
+
+    ``q/k/v_bmm_quantizer`` fake-quantise the query / key / value states handed to the attention
+    function (after RoPE and the KV-cache update, as the reference); they are per-tensor HIP
+    passes that read the transposed ``[B, H, S, D]`` states in place (no ``.contiguous()`` copy).
+    ``p_bmm_quantizer`` fake-quantises the softmax probabilities: the reference fuses that into a
+    Triton flash-attention kernel (causal) or wraps ``F.softmax`` in the eager attention
+    (non-causal); here both cases run the module's eager attention with the quantised softmax."""
+
+    def _setup(self):
+        self.q_bmm_quantizer = TensorQuantizer()
+        self.k_bmm_quantizer = TensorQuantizer()
+        self.v_bmm_quantizer = TensorQuantizer()
+        self.p_bmm_quantizer = TensorQuantizer()
+
+    @staticmethod
+    def get_attn_type(attn_module) -> type:
+        return getattr(attn_module, "_original_cls", type(attn_module))
+
+    @staticmethod
+    def is_compatible_attention(attn_cls) -> bool:
+        mod = inspect.getmodule(attn_cls)
+        return getattr(mod, "ALL_ATTENTION_FUNCTIONS", None) is not None
+
+    def _eager_p_qdq_attention(self, eager_fn, query_states, key_states, value_states, *args, **kwargs):
+        pq = self.p_bmm_quantizer
+        orig_softmax = torch.nn.functional.softmax
+
+        def _quantized_softmax(*s_args, **s_kwargs):
+            return pq(orig_softmax(*s_args, **s_kwargs))
+
+        with _replace_function(torch.nn.functional, "softmax", _quantized_softmax):
+            return eager_fn(self, query_states, key_states, value_states, *args, **kwargs)
+
+    @staticmethod
+    def _quantized_attention(original_attention_interface, eager_fn, self, query_states, key_states,
+                             value_states, *args, **kwargs):
+        query_states = self.q_bmm_quantizer(query_states)
+        key_states = self.k_bmm_quantizer(key_states)
+        value_states = self.v_bmm_quantizer(value_states)
+        if self.p_bmm_quantizer.is_enabled:
+            return self._eager_p_qdq_attention(eager_fn, query_states, key_states, value_states, *args, **kwargs)
+        return original_attention_interface(self, query_states, key_states, value_states, *args, **kwargs)
+
+    def forward(self, *args, **kwargs):
+        cfg = getattr(self, "config", None)
+        if cfg is None:
+            cfg = next((getattr(m, "config", None) for m in self.children() if hasattr(m, "config")), None)
+        impl = getattr(cfg, "_attn_implementation", None) if cfg is not None else None
+        eager = impl is None or impl == "eager" or (impl == "sdpa" and kwargs.get("output_attentions", False))
+        module = inspect.getmodule(self.get_attn_type(self))
+        eager_fn = getattr(module, "eager_attention_forward", None)
+        if eager:
+            if eager_fn is None:
+                raise AssertionError(
+                    f"Module {module} does not have `eager_attention_forward` to enable KV Cache quantization. "
+                    "Please use a different attention implementation such as `sdpa`."
+                )
+            original = eager_fn
+        else:
+            original = module.ALL_ATTENTION_FUNCTIONS[impl]
+        if self.p_bmm_quantizer.is_enabled and eager_fn is None:
+            raise NotImplementedError(f"p_bmm_quantizer needs the eager attention of {module}")
+        patch_fn = functools.partial(self._quantized_attention, original, eager_fn)
+        registry = module.ALL_ATTENTION_FUNCTIONS
+        had_local = (not eager) and impl in registry._local_mapping
+        if eager:
+            module.eager_attention_forward = patch_fn
+        else:
+            registry[impl] = patch_fn
+        try:
+            return self._original_cls.forward(self, *args, **kwargs)
+        finally:
+            if eager:
+                module.eager_attention_forward = original
+            elif had_local:
+                registry[impl] = original
+            else:
+                del registry[impl]
+
+
+def _wraps_nested_attention(module) -> bool:
+    return any(type(c).__name__.endswith("Attention") for c in module.children())
+
+
+@register_on_the_fly
+def register_hf_attentions_on_the_fly(model):
+    """Register the transformers attention classes of ``model`` for KV-cache / BMM quantization
+    (reference :412-460)."""
+    if not _is_hf_model(model):
+        return
+    for _, module in model.named_modules():
+        if not type(module).__name__.endswith("Attention") or _wraps_nested_attention(module):
+            continue
+        t = _QuantAttention.get_attn_type(module)
+        if t in QuantModuleRegistry or not _QuantAttention.is_compatible_attention(t):
+            continue
+        QuantModuleRegistry.register({t: f"hf.{t.__name__}"})(_QuantAttention)
+        print(f"Registered {t} to {_QuantAttention.__name__} for KV Cache quantization")
 
 
 def _is_hf_model(model) -> bool:

@@ -40,6 +40,19 @@ def _norm_axes(axis, ndim):
     return sorted({a + ndim if a < 0 else a for a in axis})
 
 
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense (the elements fill one contiguous storage range)."""
+    if t.numel() == 0:
+        return False
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
 def amax_view(input: torch.Tensor, reduce_axis) -> tuple[torch.Tensor, int, int, int, list[int]]:
     """Map a reduction to the kernel's [P, K, Q] view.
 
@@ -48,6 +61,9 @@ def amax_view(input: torch.Tensor, reduce_axis) -> tuple[torch.Tensor, int, int,
     ``keep_shape`` is the keepdims output shape.
     """
     nd = input.dim()
+    if reduce_axis is None and not input.is_contiguous() and _dense(input):
+        # per-tensor max is layout-free: read a dense strided tensor in storage order
+        return input.as_strided((input.numel(),), (1,)), 1, 1, input.numel(), [1] * nd
     if reduce_axis is None:
         red = list(range(nd))
     else:

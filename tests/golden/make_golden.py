@@ -688,6 +688,66 @@ def gen_awq_clip():
     (OUT / "awq_clip.json").write_text(json.dumps(meta, indent=1))
 
 
+def kv_cfg(name):
+    """FP8 weights/activations plus the attention BMM quantizers of each KV case."""
+    import copy
+
+    cfg = copy.deepcopy(mtq.FP8_DEFAULT_CFG)
+    fp8 = {"num_bits": (4, 3), "axis": None}
+    extra = {
+        "fp8_kv": [{"quantizer_name": "*[kv]_bmm_quantizer", "cfg": dict(fp8)}],
+        "fp8_kv_cast": [{"quantizer_name": "*[kv]_bmm_quantizer", "cfg": dict(fp8, use_constant_amax=True)}],
+        "qkv_fp8": [{"quantizer_name": "*[qkv]_bmm_quantizer", "cfg": dict(fp8)}],
+        "int8_kv": [{"quantizer_name": "*[kv]_bmm_quantizer", "cfg": {"num_bits": 8, "axis": None}}],
+    }[name]
+    cfg["quant_cfg"] = cfg["quant_cfg"] + extra
+    return cfg
+
+
+def gen_kv():
+    """KV-cache / attention BMM quantizers (plugins/huggingface.py:78-410 _QuantAttention): tiny
+    Llama (sdpa attention) with FP8 W/A plus FP8 K/V (calibrated and constant-amax "cast"), FP8
+    Q/K/V, INT8 K/V: every quantizer amax, logits, and the unified HF export (k_scale / v_scale,
+    kv_cache_quant_algo)."""
+    import tempfile
+
+    from safetensors.torch import load_file
+
+    from modelopt.torch.export import export_hf_checkpoint
+
+    g = torch.Generator().manual_seed(85)
+    ids = torch.randint(0, 32, (3, 2, 16), generator=g)
+    test = torch.randint(0, 32, (2, 16), generator=g)
+    t, meta = {"calib_ids": ids, "test_ids": test}, {}
+    for name in ["fp8_kv", "fp8_kv_cast", "qkv_fp8", "int8_kv"]:
+        m = tiny_llama_export()
+        mtq.quantize(m, kv_cfg(name), lambda mm: [mm(b) for b in ids])
+        for k, v in m.state_dict().items():
+            t[f"{name}.state.{k}"] = v.detach().clone().contiguous()
+        enabled = []
+        for n, q in m.named_modules():
+            if isinstance(q, TensorQuantizer) and q.is_enabled:
+                enabled.append(n)
+                if getattr(q, "_amax", None) is not None:
+                    t[f"{name}.amax.{n}"] = q._amax.clone().contiguous()
+        with torch.no_grad():
+            t[f"{name}.logits"] = m(test).logits.detach()
+        meta[name] = {"enabled": enabled}
+        if name in ("fp8_kv", "fp8_kv_cast"):
+            with tempfile.TemporaryDirectory() as d:
+                export_hf_checkpoint(m, export_dir=d)
+                for k, v in load_file(os.path.join(d, "model.safetensors")).items():
+                    t[f"{name}.export.{k}"] = v.contiguous()
+                hq = json.load(open(os.path.join(d, "hf_quant_config.json")))
+                cq = json.load(open(os.path.join(d, "config.json"))).get("quantization_config")
+            hq["producer"]["version"] = None
+            if cq and "producer" in cq:
+                cq["producer"]["version"] = None
+            meta[name].update(hf_quant_config=hq, quantization_config=cq)
+    save_file(t, str(OUT / "kv.safetensors"))
+    (OUT / "kv.json").write_text(json.dumps(meta, indent=1))
+
+
 def gen_presets():
     names = [
         "INT8_DEFAULT_CFG", "INT8_WEIGHT_ONLY_CFG", "FP8_DEFAULT_CFG", "FP8_PER_CHANNEL_PER_TOKEN_CFG",
@@ -695,7 +755,7 @@ def gen_presets():
         "MXFP8_DEFAULT_CFG", "MXFP6_DEFAULT_CFG", "MXFP4_DEFAULT_CFG", "MXINT8_DEFAULT_CFG",
         "W4A8_MXFP4_FP8_CFG", "MXFP4_MLP_WEIGHT_ONLY_CFG", "NVFP4_DEFAULT_CFG", "NVFP4_AWQ_LITE_CFG",
         "W4A8_AWQ_BETA_CFG", "FP8_KV_CFG", "NVFP4_KV_CFG", "NVFP4_AWQ_CLIP_CFG", "NVFP4_AWQ_FULL_CFG",
-        "NVFP4_W4A4_WEIGHT_MSE_FP8_SWEEP_CFG",
+        "NVFP4_W4A4_WEIGHT_MSE_FP8_SWEEP_CFG", "FP8_AFFINE_KV_CFG", "NVFP4_AFFINE_KV_CFG", "NVFP4_FP8_MHA_CONFIG",
     ]
 
     def enc(o):
@@ -742,7 +802,7 @@ def gen_mx_kat():
 
 
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "export", "awq", "mse", "awq_clip", "presets", "mx_kat"]
+    steps = sys.argv[1:] or ["tensor_quant", "quantizer", "calib", "mtq_linear", "llama_fp8", "mixtral_fp8", "nvfp4", "export", "awq", "mse", "awq_clip", "kv", "presets", "mx_kat"]
     for s in steps:
         print("generating", s, flush=True)
         globals()["gen_" + s]()

@@ -138,11 +138,11 @@ def _tiny_mixtral():
 
 def test_fused_experts_conversion_matches_reference():
     """C5 structure: the fused-experts plugin registers on the fly and yields the reference's
-    enabled quantizer set under FP8_DEFAULT_CFG (tests/golden/mixtral_fp8.json).  The reference's
-    KV-cache bmm quantizers (disabled under this config) are not built here."""
+    quantizer set under FP8_DEFAULT_CFG (tests/golden/mixtral_fp8.json), including the attention
+    q/k/v/p bmm quantizers (registered on the fly, disabled under this config)."""
     ref = json.loads((G / "mixtral_fp8.json").read_text())["quantizers"]
     want_enabled = {n for n, e in ref if e}
-    want_all = {n for n, _ in ref if "_bmm_quantizer" not in n}
+    want_all = {n for n, _ in ref}
     m = _tiny_mixtral()
     m.config._experts_implementation = "grouped_mm"
     mtq.conversion.replace_quant_module(m)
