@@ -134,7 +134,15 @@ def kernel_suite(ops, xs, steps, warmup):
         "export_int4_pack": (lambda x: ops.export_int4(x, i4_s), 2.5),
         "export_mxfp4_pack": (lambda x: ops.export_mxfp4(x, 32)[0], 2.5),
         "amax_per_tensor": (None, 2),
+        # K6 per-row (axis 0 kept) and per-column (axis -1 kept) running amax, K7 histogram
+        "amax_per_row": (lambda x: ops.amax_accumulate(x, acc_r, 1, x.shape[0], x.shape[1]) or acc_r, 2),
+        "amax_per_column": (lambda x: ops.amax_accumulate(x, acc_c, x.shape[0], x.shape[1], 1) or acc_c, 2),
+        "histogram_2048_abs": (lambda x: ops.histogram_abs_accumulate(x, hmax, counts, 2048, False) or counts, 2),
     }
+    acc_r = torch.zeros(xs[0].shape[0], device="cuda")
+    acc_c = torch.zeros(xs[0].shape[1], device="cuda")
+    hmax = torch.tensor([16.0 * 6], device="cuda")
+    counts = torch.zeros(2048, dtype=torch.int32, device="cuda")
     nv_bs = torch.ones(xs[0].numel() // 16, device="cuda")
     i4_s = torch.full((xs[0].shape[0], xs[0].shape[1] // 128), 0.01, device="cuda")
     acc = torch.zeros(1, device="cuda")
@@ -179,6 +187,61 @@ def cpu_baseline(target_s: float = 10.0):
         "kind": "port",
         "sample": f"{passes} passes of FP8 e4m3 static block-128 fake-quant (oracle fp8_eager, the "
         f"reference _fp8_eager ATen sequence) over bf16 [{rows}, {HIDDEN}], {el:.1f} s",
+    }
+
+
+def cpu_e2e_baseline(samples: int = 8):
+    """SURVEY §8d E2E CPU baseline: one Llama-3-8B decoder layer (bf16, random init), max
+    calibration of its 7 linears (input amax per batch + weight amax, the oracle's reduce_amax =
+    the reference ATen sequence) over `samples` x 512 tokens on the host cores; reported per layer
+    per sample, with the full 32-layer x 512-sample extrapolation labelled as such."""
+    from transformers import LlamaConfig
+    from transformers.models.llama.modeling_llama import LlamaDecoderLayer, LlamaRotaryEmbedding
+
+    from oracle import ref_ops as R  # test infrastructure: the CPU baseline only
+
+    from scripts.ptq_llama import LLAMA3_8B
+
+    cfg = LlamaConfig(**LLAMA3_8B)
+    cfg._attn_implementation = "sdpa"
+    torch.manual_seed(1234)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    try:
+        layer = LlamaDecoderLayer(cfg, 0).eval()
+        rope = LlamaRotaryEmbedding(cfg)
+    finally:
+        torch.set_default_dtype(prev)
+    amax = {}
+
+    def hook(mod, args):
+        a = R.reduce_amax(args[0], axis=None)
+        amax[mod] = a if mod not in amax else torch.maximum(amax[mod], a)
+        if ("w", mod) not in amax:
+            amax[("w", mod)] = R.reduce_amax(mod.weight, axis=None)
+
+    hs = [m.register_forward_pre_hook(hook) for m in layer.modules() if isinstance(m, torch.nn.Linear)]
+    g = torch.Generator().manual_seed(1234)
+    x = (torch.randn(samples, 512, cfg.hidden_size, generator=g) * 0.5).to(torch.bfloat16)
+    pos = torch.arange(512)[None].expand(samples, -1)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        pe = rope(x, pos)
+        for i in range(0, samples, 4):
+            layer(x[i : i + 4], position_embeddings=(pe[0][i : i + 4], pe[1][i : i + 4]), attention_mask=None)
+    el = time.perf_counter() - t0
+    for h in hs:
+        h.remove()
+    per = el / samples
+    return {
+        "value": round(per, 4),
+        "unit": "s per decoder layer per 512-token sample",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"Llama-3-8B decoder layer, bf16, {samples} x 512 tokens, max calibration of 7 linears "
+        f"(oracle reduce_amax), {el:.1f} s",
+        "extrapolated_ptq_wall_clock_s": round(per * 32 * 512, 1),
+        "extrapolation": "per-layer-per-sample x 32 layers x 512 samples (labelled estimate, not run)",
     }
 
 
@@ -273,6 +336,8 @@ def main():
         out["ptq"] = res
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if not args.no_ptq:
+            out["cpu_baseline"]["ptq_e2e"] = cpu_e2e_baseline()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import contextlib
 import fnmatch
+import functools
 import re
 from collections.abc import Callable
 from typing import Any
@@ -12,7 +13,7 @@ import torch.nn as nn
 
 from .config import QuantizeConfig, QuantizerAttributeConfig, normalize_quant_cfg_list
 from .nn.modules.quant_module import QuantModule, QuantModuleRegistry
-from .nn.modules.tensor_quantizer import SequentialQuantizer, TensorQuantizer
+from .nn.modules.tensor_quantizer import SequentialQuantizer, TensorQuantizer, _AttributeItems
 from .utils.names import is_quantized
 
 __all__ = [
@@ -83,15 +84,28 @@ def _normalize_fused_experts_quantizer_name(name: str) -> str:
     return _FUSED_EXPERTS_QUANTIZER_LIST_RE.sub(lambda m: m.group(1).removesuffix("s"), name)
 
 
+@functools.lru_cache(maxsize=4096)
+def _wildcard_re(pattern: str):
+    return re.compile(fnmatch.translate(pattern))
+
+
+@functools.lru_cache(maxsize=65536)
+def _normalized_name(name: str) -> str:
+    return _normalize_fused_experts_quantizer_name(name)
+
+
+def _quantizer_items(model: nn.Module):
+    """The (name, quantizer) pairs of ``model``: the only modules a quant_cfg entry can match."""
+    return [(n, m) for n, m in model.named_modules() if isinstance(m, (TensorQuantizer, SequentialQuantizer))]
+
+
 def _match_quantizer(wildcard_or_filter_func, name, module, parent_class, full_model) -> bool:
     if not isinstance(module, (TensorQuantizer, SequentialQuantizer)):
         return False
     if isinstance(wildcard_or_filter_func, str):
-        normalized = _normalize_fused_experts_quantizer_name(name)
-        if not (
-            fnmatch.fnmatch(name, wildcard_or_filter_func)
-            or (normalized != name and fnmatch.fnmatch(normalized, wildcard_or_filter_func))
-        ):
+        rx = _wildcard_re(wildcard_or_filter_func)
+        normalized = _normalized_name(name)
+        if not (rx.match(name) or (normalized != name and rx.match(normalized))):
             return False
     elif callable(wildcard_or_filter_func):
         if not wildcard_or_filter_func(name):
@@ -106,6 +120,7 @@ def _match_quantizer(wildcard_or_filter_func, name, module, parent_class, full_m
 def set_quantizer_by_cfg(quant_model: nn.Module, quant_cfg):
     """Apply an ordered quant_cfg list (reference :245-314): later entries win; an entry with
     ``cfg`` fully replaces the attributes, an ``enable``-only entry toggles."""
+    qitems = [_quantizer_items(quant_model)]  # refreshed when a full entry swaps quantizer types
     for entry in normalize_quant_cfg_list(quant_cfg):
         name = entry["quantizer_name"]
         cfg = entry["cfg"]
@@ -121,7 +136,7 @@ def set_quantizer_by_cfg(quant_model: nn.Module, quant_cfg):
         else:
             parent_class = None
         if cfg is None:
-            set_quantizer_attributes_partial(quant_model, name, {"enable": enable}, parent_class)
+            set_quantizer_attributes_partial(quant_model, name, {"enable": enable}, parent_class, _items=qitems[0])
         else:
             if isinstance(cfg, QuantizerAttributeConfig):
                 attributes = cfg.model_copy(update={"enable": enable})
@@ -134,37 +149,47 @@ def set_quantizer_by_cfg(quant_model: nn.Module, quant_cfg):
                     else QuantizerAttributeConfig(**c, enable=enable)
                     for c in cfg
                 ]
-            set_quantizer_attributes_full(quant_model, name, attributes, parent_class)
+            if set_quantizer_attributes_full(quant_model, name, attributes, parent_class, _items=qitems[0]):
+                qitems[0] = _quantizer_items(quant_model)
 
 
-def set_quantizer_attributes_full(quant_model, wildcard_or_filter_func, attributes, parent_class=None):
-    """Fully replace matched quantizers' attributes (reference :373-440)."""
+def set_quantizer_attributes_full(quant_model, wildcard_or_filter_func, attributes, parent_class=None,
+                                  _items=None) -> bool:
+    """Fully replace matched quantizers' attributes (reference :373-440).  Returns whether a
+    quantizer module was swapped (TensorQuantizer <-> SequentialQuantizer)."""
     if not isinstance(attributes, (QuantizerAttributeConfig, list)):
         raise ValueError(f"Invalid type for attributes: {type(attributes)}")
-    for name, module in list(quant_model.named_modules()):
+    # validated once, applied to every matched quantizer
+    applied = (
+        [_AttributeItems(a.items()) for a in attributes]
+        if isinstance(attributes, list)
+        else _AttributeItems(attributes.items())
+    )
+    swapped = False
+    for name, module in list(_items if _items is not None else quant_model.named_modules()):
         if not _match_quantizer(wildcard_or_filter_func, name, module, parent_class, quant_model):
             continue
         if isinstance(attributes, list):
-            if not isinstance(module, SequentialQuantizer):
+            if not isinstance(module, SequentialQuantizer) or len(attributes) != len(module):
                 parent = quant_model.get_submodule(name.rpartition(".")[0])
                 module = SequentialQuantizer(*(TensorQuantizer() for _ in range(len(attributes))))
                 setattr(parent, name.rpartition(".")[-1], module)
-            elif len(attributes) != len(module):
-                parent = quant_model.get_submodule(name.rpartition(".")[0])
-                module = SequentialQuantizer(*(TensorQuantizer() for _ in range(len(attributes))))
-                setattr(parent, name.rpartition(".")[-1], module)
-            module.set_from_attribute_config(attributes)
+                swapped = True
+            module.set_from_attribute_config(applied)
         else:
             if isinstance(module, SequentialQuantizer):
                 parent = quant_model.get_submodule(name.rpartition(".")[0])
                 module = TensorQuantizer()
                 setattr(parent, name.rpartition(".")[-1], module)
-            module.set_from_attribute_config(attributes)
+                swapped = True
+            module.set_from_attribute_config(applied)
+    return swapped
 
 
-def set_quantizer_attributes_partial(quant_model, wildcard_or_filter_func, partial: dict, parent_class=None):
+def set_quantizer_attributes_partial(quant_model, wildcard_or_filter_func, partial: dict, parent_class=None,
+                                     _items=None):
     """Update only the given attributes of matched quantizers (reference :443-505)."""
-    for name, module in quant_model.named_modules():
+    for name, module in _items if _items is not None else quant_model.named_modules():
         if _match_quantizer(wildcard_or_filter_func, name, module, parent_class, quant_model):
             if isinstance(module, SequentialQuantizer):
                 for q in module:

@@ -18,6 +18,7 @@ MI355X-specific behaviour:
 from __future__ import annotations
 
 import contextlib
+import copy
 import math
 import warnings
 from collections.abc import Callable
@@ -87,6 +88,28 @@ def _standardize_constructor_args(val):
     raise TypeError(f"Unsupported calibrator constructor {val!r}")
 
 
+class _AttributeItems:
+    """A validated attribute list applied to many quantizers: pydantic validation once, a fresh
+    copy of mutable values per quantizer."""
+
+    __slots__ = ("_items",)
+
+    def __init__(self, items):
+        self._items = list(items)
+
+    def fresh(self):
+        return [(k, copy.deepcopy(v) if isinstance(v, (dict, list)) else v) for k, v in self._items]
+
+
+_DEFAULT_ITEMS: list = []
+
+
+def _default_attribute_items() -> _AttributeItems:
+    if not _DEFAULT_ITEMS:
+        _DEFAULT_ITEMS.append(_AttributeItems(QuantizerAttributeConfig().items()))
+    return _DEFAULT_ITEMS[0]
+
+
 class TensorQuantizer(nn.Module):
     """Tensor quantizer module (reference :136)."""
 
@@ -106,9 +129,8 @@ class TensorQuantizer(nn.Module):
 
     def __init__(self, quant_attribute_cfg=None, if_quant=True, if_calib=False, amax=None):
         super().__init__()
-        quant_attribute_cfg = (
-            quant_attribute_cfg if quant_attribute_cfg is not None else QuantizerAttributeConfig()
-        )
+        if quant_attribute_cfg is None:
+            quant_attribute_cfg = _default_attribute_items()
         if amax is not None:
             self.amax = amax
         self._use_constant_amax = False
@@ -125,7 +147,9 @@ class TensorQuantizer(nn.Module):
     # ---- configuration --------------------------------------------------------------------
     def set_from_attribute_config(self, attribute_cfg: QuantizerAttributeConfig | dict[str, Any]):
         """Set quantizer attributes from attribute_cfg (reference :228-290)."""
-        if isinstance(attribute_cfg, dict) and set(attribute_cfg) == {"enable"}:
+        if isinstance(attribute_cfg, _AttributeItems):
+            items = attribute_cfg.fresh()
+        elif isinstance(attribute_cfg, dict) and set(attribute_cfg) == {"enable"}:
             # a bare enable toggle (set_quantizer_by_cfg enable entries, contexts): the reference
             # applies dict attributes unvalidated, so {"enable": True} is legal here
             items = attribute_cfg.items()
@@ -182,13 +206,28 @@ class TensorQuantizer(nn.Module):
                 f"{attribute} is not a valid `TensorQuantizer` attribute"
             )
             name, setter = custom.get(attribute, (f"_{attribute}", lambda v: v))
-            setattr(self, name, setter(val))
+            self._set_plain(name, setter(val))
         if self._rotate_enabled():
             raise NotImplementedError("modelopt_amd: input rotation (QuaRot/SpinQuant) is out of scope")
         if getattr(self, "_bias", None):
             raise NotImplementedError("modelopt_amd: affine bias calibration is out of scope")
         if self.is_mx_format:
             self._pass_through_bwd = True
+
+    def _set_plain(self, name, value):
+        """``setattr`` without nn.Module's per-call parameter/buffer/module bookkeeping for plain
+        values (a model conversion sets ~20 attributes on each of ~800 quantizers)."""
+        d = self.__dict__
+        if (
+            isinstance(value, (torch.Tensor, nn.Module))
+            or name in d["_parameters"]
+            or name in d["_buffers"]
+            or name in d["_modules"]
+            or isinstance(getattr(type(self), name, None), property)
+        ):
+            setattr(self, name, value)
+        else:
+            d[name] = value
 
     def _rotate_enabled(self):
         r = getattr(self, "_rotate", False)
