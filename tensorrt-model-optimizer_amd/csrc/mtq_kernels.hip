@@ -12,6 +12,7 @@
 #include <string.h>
 #include <math.h>
 #include <stdlib.h>
+#include <type_traits>
 
 #include "mtq_amd.h"
 #include "mtq_device.hpp"
@@ -688,6 +689,318 @@ __global__ __launch_bounds__(kThreads) void amax_generic_kernel(const T *__restr
   }
 }
 
+int env_variant(const char *name, int *cache) {
+  if (*cache < 0) {
+    const char *e = getenv(name);
+    *cache = e ? atoi(e) : 0;
+  }
+  return *cache;
+}
+
+// Rows, unrolled form: one item = (row, chunk of <= G*U vectors) per group of G lanes, U
+// non-temporal 16 B loads in flight per lane, one chunk per group (no grid-stride loop, the
+// structure that reaches ~6 TB/s in ew_vec_kernel).  With one chunk per row and P == 1 every
+// output word has exactly one writer in the launch, so the fold is a plain load-max-store
+// instead of an atomic (R atomics to distinct words still cost ~10 us at R = 32k).
+template <typename T, int G, int U, bool EXCL>
+__global__ __launch_bounds__(kThreads) void amax_rows_u_kernel(const T *__restrict__ x,
+                                                                int64_t R, int64_t Q, int64_t K,
+                                                                int64_t chunks, uint32_t *out) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t qvec = Q / N;
+  const int64_t item = (int64_t)blockIdx.x * (kThreads / G) + threadIdx.x / G;
+  if (item >= R * chunks) return;  // whole G-lane groups exit together
+  const int gl = threadIdx.x % G;
+  const int64_t r = item / chunks, c = item - r * chunks;
+  const int64_t v0 = c * (int64_t)(G * U);
+  int64_t v1 = v0 + G * U;
+  v1 = v1 < qvec ? v1 : qvec;
+  const T *row = x + r * Q;
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = v0 + gl + u * G;
+    if (i < v1)
+      v[u] = ldg_vec_nt(row + i * N);
+    else
+      v[u].raw = make_uint4(0, 0, 0, 0);
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    uint32_t b = vec_absmax_bits(v[u]);
+    m = b > m ? b : m;
+  }
+  m = group_max_u32<G>(m);
+  if (gl == 0) {
+    if (EXCL) {
+      uint32_t o = out[r];
+      out[r] = m > o ? m : o;
+    } else {
+      atomicMax(out + (r % K), m);
+    }
+  }
+}
+
+// Columns, LDS form: x viewed as [P, K] (K % N == 0); a block owns a chunk of `lpr` column
+// vectors (lpr <= kThreads lanes across a row, kThreads / lpr row lanes) and a slab of rows,
+// keeps U loads in flight per lane, folds its row lanes in LDS and issues one atomicMax per
+// column.  The old form (one slab per lane, N atomics per lane) spent most of its time in
+// ~2 M same-address atomics at [32768, 4096].
+template <typename T, int U>
+__global__ __launch_bounds__(kThreads) void amax_cols_lds_kernel(const T *__restrict__ x,
+                                                                  int64_t P, int64_t K, int lpr,
+                                                                  int64_t nchunks,
+                                                                  int64_t rows_per_slab,
+                                                                  uint32_t *out) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  __shared__ uint32_t sh[kThreads * N];
+  const int64_t kvec = K / N;
+  const int64_t chunk = blockIdx.x % nchunks, slab = blockIdx.x / nchunks;
+  const int tc = threadIdx.x % lpr, tr = threadIdx.x / lpr;
+  const int rstep = kThreads / lpr;
+  const int64_t kv = chunk * lpr + tc;
+  const bool active = tr < rstep && kv < kvec;
+  if (rstep > 1) {
+    for (int i = threadIdx.x; i < lpr * N; i += kThreads) sh[i] = 0;
+    __syncthreads();
+  }
+  uint32_t m[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) m[j] = 0;
+  if (active) {
+    const int64_t p0 = slab * rows_per_slab;
+    int64_t p1 = p0 + rows_per_slab;
+    p1 = p1 < P ? p1 : P;
+    const T *base = x + kv * N;
+    int64_t p = p0 + tr;
+    for (; p + (int64_t)(U - 1) * rstep < p1; p += (int64_t)U * rstep) {
+      V v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ldg_vec_nt(base + (p + (int64_t)u * rstep) * K);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          uint32_t b = abs_bits_t<T>(v[u].e[j]);
+          m[j] = b > m[j] ? b : m[j];
+        }
+    }
+    for (; p < p1; p += rstep) {
+      V v = ldg_vec_nt(base + p * K);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        uint32_t b = abs_bits_t<T>(v.e[j]);
+        m[j] = b > m[j] ? b : m[j];
+      }
+    }
+  }
+  if (rstep == 1) {
+    if (active)
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (m[j]) atomicMax(out + kv * N + j, m[j]);
+    return;
+  }
+  if (active)
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (m[j]) atomicMax(sh + tc * N + j, m[j]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < lpr * N; i += kThreads) {
+    const int64_t col = chunk * lpr * N + i;
+    if (col < K && sh[i]) atomicMax(out + col, sh[i]);
+  }
+}
+
+// Columns, wide form: 1024-thread blocks, `lpr` (<= 64) lanes across a column chunk and
+// 1024 / lpr row lanes, U loads in flight per lane; row lanes fold in LDS, then one atomicMax
+// per column per block.  Global atomics cost ~30 ns per thousand on gfx950 (measured: 1 M of
+// them add ~35 us to a 44 us read), so the grid is kept to O(CUs) blocks and the atomic count
+// to slabs x K with few slabs; 16 waves per block keep ~128 KB in flight per CU.
+constexpr int kColsThreads = 1024;
+template <typename T, int U>
+__global__ __launch_bounds__(kColsThreads) void amax_cols_wide_kernel(
+    const T *__restrict__ x, int64_t P, int64_t K, int lpr, int64_t nchunks,
+    int64_t rows_per_slab, uint32_t *out) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  __shared__ uint32_t sh[64 * N];
+  const int64_t kvec = K / N;
+  const int64_t chunk = blockIdx.x % nchunks, slab = blockIdx.x / nchunks;
+  const int tc = threadIdx.x % lpr, tr = threadIdx.x / lpr;
+  const int rstep = kColsThreads / lpr;
+  const int64_t kv = chunk * lpr + tc;
+  const bool active = kv < kvec;
+  for (int i = threadIdx.x; i < lpr * N; i += kColsThreads) sh[i] = 0;
+  __syncthreads();
+  uint32_t m[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) m[j] = 0;
+  if (active) {
+    const int64_t p0 = slab * rows_per_slab;
+    int64_t p1 = p0 + rows_per_slab;
+    p1 = p1 < P ? p1 : P;
+    const T *base = x + kv * N;
+    int64_t p = p0 + tr;
+    for (; p + (int64_t)(U - 1) * rstep < p1; p += (int64_t)U * rstep) {
+      V v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ldg_vec_nt(base + (p + (int64_t)u * rstep) * K);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          uint32_t b = abs_bits_t<T>(v[u].e[j]);
+          m[j] = b > m[j] ? b : m[j];
+        }
+    }
+    for (; p < p1; p += rstep) {
+      V v = ldg_vec_nt(base + p * K);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        uint32_t b = abs_bits_t<T>(v.e[j]);
+        m[j] = b > m[j] ? b : m[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (m[j]) atomicMax(sh + tc * N + j, m[j]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < lpr * N; i += kColsThreads) {
+    const int64_t col = chunk * lpr * N + i;
+    if (col < K && sh[i]) atomicMax(out + col, sh[i]);
+  }
+}
+
+template <typename T>
+int launch_amax_cols_wide(const T *x, int64_t P, int64_t K, uint32_t *out, int blocks_per_2cu,
+                          hipStream_t stream) {
+  constexpr int N = Vec<T>::N, U = 8;
+  const int64_t kvec = K / N;
+  const int lpr = (int)(kvec < 64 ? kvec : 64);
+  const int64_t nchunks = (kvec + lpr - 1) / lpr;
+  const int rstep = kColsThreads / lpr;
+  // blocks_per_2cu == 0: 1 block per CU when every row lane then gets >= 4 unrolled rounds,
+  // else 2 (measured: [32768, 4096] 45 vs 53 us, [8192, 4096] 19.7 vs 16.0 us).  The slab
+  // count is rounded down so that the grid never spills a partial second round of blocks.
+  if (blocks_per_2cu == 0) {
+    const int64_t slabs1 = (int64_t)num_cus() / nchunks;
+    blocks_per_2cu = (slabs1 >= 1 && P / slabs1 >= (int64_t)4 * U * rstep) ? 2 : 4;
+  }
+  const int64_t want = (int64_t)num_cus() * blocks_per_2cu / 2;
+  int64_t slabs = want / nchunks;
+  const int64_t max_slabs = (P + (int64_t)U * rstep - 1) / ((int64_t)U * rstep);
+  if (slabs > max_slabs) slabs = max_slabs;
+  if (slabs < 1) slabs = 1;
+  const int64_t rows_per_slab = (P + slabs - 1) / slabs;
+  slabs = (P + rows_per_slab - 1) / rows_per_slab;
+  const unsigned g = (unsigned)(nchunks * slabs);
+  amax_cols_wide_kernel<T, U><<<g, kColsThreads, 0, stream>>>(x, P, K, lpr, nchunks,
+                                                              rows_per_slab, out);
+  return check_launch();
+}
+
+// Short rows (Q / N <= 64 vectors, e.g. the [rows * K / 128, 128] block view): a group of G
+// lanes covers one row, and each group takes RU consecutive rows with one load per row in
+// flight per lane; in exclusive mode the accumulator words are fetched before the data so
+// their latency overlaps it.
+template <typename T, int G, int RU, bool EXCL>
+__global__ __launch_bounds__(kThreads) void amax_rows_short_kernel(const T *__restrict__ x,
+                                                                    int64_t R, int64_t Q,
+                                                                    int64_t K, uint32_t *out) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const int64_t qvec = Q / N;
+  const int64_t r0 = ((int64_t)blockIdx.x * (kThreads / G) + threadIdx.x / G) * RU;
+  if (r0 >= R) return;
+  const int gl = threadIdx.x % G;
+  uint32_t o[RU];
+  if (EXCL && gl == 0) {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) o[u] = r0 + u < R ? out[r0 + u] : 0;
+  }
+  V v[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    if (r0 + u < R && gl < qvec)
+      v[u] = ldg_vec_nt(x + (r0 + u) * Q + (int64_t)gl * N);
+    else
+      v[u].raw = make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    uint32_t m = group_max_u32<G>(vec_absmax_bits(v[u]));
+    if (gl == 0 && r0 + u < R) {
+      if (EXCL)
+        out[r0 + u] = m > o[u] ? m : o[u];
+      else
+        atomicMax(out + ((r0 + u) % K), m);
+    }
+  }
+}
+
+template <typename T>
+int launch_amax_rows_u(const T *x, int64_t P, int64_t K, int64_t Q, uint32_t *out,
+                       hipStream_t stream) {
+  constexpr int N = Vec<T>::N;
+  const int64_t R = P * K, qvec = Q / N;
+  if (qvec >= 64) {
+    constexpr int G = 64, U = 8;
+    const int64_t chunks = (qvec + G * U - 1) / (G * U);
+    const int64_t items = R * chunks;
+    const unsigned g = (unsigned)((items + kThreads / G - 1) / (kThreads / G));
+    if (chunks == 1 && P == 1)
+      amax_rows_u_kernel<T, G, U, true><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunks, out);
+    else
+      amax_rows_u_kernel<T, G, U, false><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunks, out);
+    return check_launch();
+  }
+  // short rows: the smallest power-of-two group covering the row, RU rows per group
+  constexpr int RU = 4;
+  auto go = [&](auto gtag) {
+    constexpr int G = decltype(gtag)::value;
+    const int64_t rows_per_block = (int64_t)(kThreads / G) * RU;
+    const unsigned g = (unsigned)((R + rows_per_block - 1) / rows_per_block);
+    if (P == 1)
+      amax_rows_short_kernel<T, G, RU, true><<<g, kThreads, 0, stream>>>(x, R, Q, K, out);
+    else
+      amax_rows_short_kernel<T, G, RU, false><<<g, kThreads, 0, stream>>>(x, R, Q, K, out);
+    return check_launch();
+  };
+  if (qvec > 32) return go(std::integral_constant<int, 64>{});
+  if (qvec > 16) return go(std::integral_constant<int, 32>{});
+  if (qvec > 8) return go(std::integral_constant<int, 16>{});
+  if (qvec > 4) return go(std::integral_constant<int, 8>{});
+  if (qvec > 2) return go(std::integral_constant<int, 4>{});
+  if (qvec > 1) return go(std::integral_constant<int, 2>{});
+  return go(std::integral_constant<int, 1>{});
+}
+
+template <typename T>
+int launch_amax_cols_lds(const T *x, int64_t P, int64_t K, uint32_t *out, int blocks_per_cu,
+                         hipStream_t stream) {
+  constexpr int N = Vec<T>::N, U = 8;
+  const int64_t kvec = K / N;
+  const int lpr = (int)(kvec < kThreads ? kvec : kThreads);
+  const int64_t nchunks = (kvec + lpr - 1) / lpr;
+  const int rstep = kThreads / lpr;
+  const int64_t want = (int64_t)num_cus() * blocks_per_cu;
+  int64_t slabs = (want + nchunks - 1) / nchunks;
+  // at least U row steps per slab so the unrolled body runs
+  const int64_t max_slabs = (P + (int64_t)U * rstep - 1) / ((int64_t)U * rstep);
+  if (slabs > max_slabs) slabs = max_slabs;
+  if (slabs < 1) slabs = 1;
+  const int64_t rows_per_slab = (P + slabs - 1) / slabs;
+  slabs = (P + rows_per_slab - 1) / rows_per_slab;
+  const unsigned g = (unsigned)(nchunks * slabs);
+  amax_cols_lds_kernel<T, U><<<g, kThreads, 0, stream>>>(x, P, K, lpr, nchunks, rows_per_slab, out);
+  return check_launch();
+}
+
 template <typename T>
 int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
                 hipStream_t stream) {
@@ -713,6 +1026,23 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
       return launch_amax_persist<T, 4>(x, n, nvec, out, 2, stream);
     default:
       return launch_amax_persist<T, 8>(x, n, nvec, out, 2, stream);
+    }
+  }
+  static int rows_v = -1, cols_v = -1;
+  if (Q % N == 0 && al && Q >= N && env_variant("MTQ_AMD_ROWS_VARIANT", &rows_v) != 1)
+    return launch_amax_rows_u<T>(x, P, K, Q, out, stream);
+  if (Q == 1 && K % N == 0 && al && env_variant("MTQ_AMD_COLS_VARIANT", &cols_v) != 1) {
+    switch (cols_v) {
+    case 2:
+      return launch_amax_cols_lds<T>(x, P, K, out, 2, stream);
+    case 3:
+      return launch_amax_cols_wide<T>(x, P, K, out, 4, stream);
+    case 4:
+      return launch_amax_cols_wide<T>(x, P, K, out, 1, stream);
+    case 5:
+      return launch_amax_cols_wide<T>(x, P, K, out, 2, stream);
+    default:
+      return launch_amax_cols_wide<T>(x, P, K, out, 0, stream);
     }
   }
   if (Q % N == 0 && al && Q >= N) {
@@ -856,6 +1186,137 @@ __global__ __launch_bounds__(kThreads) void hist_vec_kernel(const T *__restrict_
     if (sh[b]) atomicAdd(counts + b, sh[b]);
 }
 
+// Replicated-LDS form: REP copies of the bins, interleaved (bin b, copy c at b*REP + c) and
+// picked by lane, so lanes of one ds_add that land in the same bin -- calibration data piles
+// into the first few dozen of 2048 bins -- hit REP different words instead of serialising on one.
+// Each block owns one contiguous chunk of vectors with U loads in flight per lane; blocks are
+// few (O(CUs)) so the flush (one global atomic per non-zero bin per block) stays cheap.
+template <typename T, int REP, int U>
+__global__ __launch_bounds__(kThreads) void hist_rep_kernel(const T *__restrict__ x, int64_t nvec,
+                                                             int64_t vec_per_block,
+                                                             const float *hmax, int bins,
+                                                             int skip_zeros, uint32_t *counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+  using V = Vec<T>;
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  const float fb = (float)bins;
+  const float span = hi - lo;
+  for (int b = threadIdx.x; b < bins * REP; b += kThreads) sh[b] = 0;
+  __syncthreads();
+  const int c = threadIdx.x % REP;
+  const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
+  int64_t v1 = v0 + vec_per_block;
+  v1 = v1 < nvec ? v1 : nvec;
+  for (int64_t i = v0 + threadIdx.x; i < v1; i += (int64_t)kThreads * U) {
+    V v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + (int64_t)u * kThreads;
+      if (k < v1)
+        v[u] = ldg_vec_nt(x + k * V::N);
+      else
+        v[u].raw = make_uint4(0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i + (int64_t)u * kThreads >= v1) continue;
+#pragma unroll
+      for (int j = 0; j < V::N; ++j) {
+        float a = fabsf(Elem<T>::ld(v[u].e[j]));
+        bool ok = (a >= lo && a <= hi) && !(skip_zeros && a == 0.f);
+        if (ok) {
+          int b = (int)(((a - lo) * fb) / span);
+          if (b == bins) b -= 1;
+          atomicAdd(sh + b * REP + c, 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < bins; b += kThreads) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < REP; ++k) s += sh[b * REP + k];
+    if (s) atomicAdd(counts + b, s);
+  }
+}
+
+// 16-bit inputs (bf16 / f16): |x| has only 2^15 bit patterns, so each block first tabulates the
+// bin of every pattern in LDS (uint16, 0xFFFF = dropped) with exactly the per-element formula
+// above (fp32 multiply, true division, truncation, last-bin clamp, range / NaN / zero checks),
+// then the stream costs a mask, one LDS table read and one LDS add per element instead of ~25
+// VALU operations (the divide dominates) -- the VALU-bound kernels above reach ~2.4 TB/s.
+// Patterns above hi are dropped without a division, so the table costs ~1-3 us per block.
+// One 1024-thread block per CU (64 KB table + up to 64 KB of bins in LDS).
+constexpr int kHistLutThreads = 1024;
+constexpr int kHistLutWords = 16384;
+template <typename T, int REP, int U>
+__global__ __launch_bounds__(kHistLutThreads) void hist_lut_kernel(
+    const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
+    int skip_zeros, uint32_t *counts) {
+  static_assert(sizeof(T) == 2, "16-bit element types only");
+  __shared__ uint16_t lut[32768];
+  __shared__ uint32_t sh[kHistLutWords];
+  using V = Vec<T>;
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  const float fb = (float)bins;
+  const float span = hi - lo;
+  for (int b = threadIdx.x; b < bins * REP; b += kHistLutThreads) sh[b] = 0;
+  for (int m = threadIdx.x; m < 32768; m += kHistLutThreads) {
+    T t;
+    uint16_t bits = (uint16_t)m;
+    memcpy(&t, &bits, 2);
+    const float a = Elem<T>::ld(t);
+    uint16_t e = 0xFFFF;
+    if ((a >= lo && a <= hi) && !(skip_zeros && a == 0.f)) {
+      int b = (int)(((a - lo) * fb) / span);
+      if (b == bins) b -= 1;
+      e = (uint16_t)b;
+    }
+    lut[m] = e;
+  }
+  __syncthreads();
+  const int c = threadIdx.x % REP;
+  const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
+  int64_t v1 = v0 + vec_per_block;
+  v1 = v1 < nvec ? v1 : nvec;
+  for (int64_t i = v0 + threadIdx.x; i < v1; i += (int64_t)kHistLutThreads * U) {
+    V v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + (int64_t)u * kHistLutThreads;
+      if (k < v1)
+        v[u] = ldg_vec_nt(x + k * V::N);
+      else
+        v[u].raw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);  // NaN: dropped
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t w[4] = {v[u].raw.x, v[u].raw.y, v[u].raw.z, v[u].raw.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t m = (w[j >> 1] >> ((j & 1) * 16)) & 0x7fffu;
+        const uint32_t b = lut[m];
+        if (b != 0xFFFFu) atomicAdd(sh + b * REP + c, 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < bins; b += kHistLutThreads) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < REP; ++k) s += sh[b * REP + k];
+    if (s) atomicAdd(counts + b, s);
+  }
+}
 
 // ============================================================================================
 // AWQ-lite search helpers: column scale (x * s[col]) and the per-alpha MSE loss
@@ -1568,6 +2029,73 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
     const T *xt = reinterpret_cast<const T *>(x);
     const bool lds = bins <= 16384;
     const size_t shm = lds ? (size_t)bins * 4 : 0;
+    static int hv = -1;
+    const int var = env_variant("MTQ_AMD_HIST_VARIANT", &hv);
+    if constexpr (sizeof(T) == 2) {
+      if ((var == 0 || var == 6 || var == 7) && aligned16(x) && n % N == 0 && bins <= kHistLutWords) {
+        int rep = var == 6 ? 1 : var == 7 ? 4 : 8;
+        while (rep > 1 && bins * rep > kHistLutWords) rep >>= 1;
+        const int64_t nvec = n / N;
+        int64_t blocks = num_cus();
+        const int64_t min_per_block = (int64_t)kHistLutThreads * 8;
+        int64_t vpb = (nvec + blocks - 1) / blocks;
+        vpb = vpb < min_per_block ? min_per_block : vpb;
+        blocks = (nvec + vpb - 1) / vpb;
+        switch (rep) {
+        case 8:
+          hist_lut_kernel<T, 8, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+          break;
+        case 4:
+          hist_lut_kernel<T, 4, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+          break;
+        case 2:
+          hist_lut_kernel<T, 2, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+          break;
+        default:
+          hist_lut_kernel<T, 1, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        }
+        return check_launch();
+      }
+    }
+    if (var != 1 && aligned16(x) && n % N == 0) {
+      // replicated-LDS form: (REP, blocks per CU) by variant; REP * bins words must fit 64 KB
+      int rep = 4, per_cu = 4;
+      if (var == 2) rep = 1;
+      if (var == 4) rep = 8, per_cu = 2;
+      if (var == 5) per_cu = 8;
+      while (rep > 1 && (int64_t)bins * rep * 4 > 65536) rep >>= 1;
+      if ((int64_t)bins * rep * 4 <= 65536) {
+        const int64_t nvec = n / N;
+        int64_t blocks = (int64_t)num_cus() * per_cu;
+        const int64_t min_per_block = (int64_t)kThreads * 4;
+        int64_t vpb = (nvec + blocks - 1) / blocks;
+        vpb = vpb < min_per_block ? min_per_block : vpb;
+        blocks = (nvec + vpb - 1) / vpb;
+        const size_t shr = (size_t)bins * rep * 4;
+        switch (rep) {
+        case 8:
+          hist_rep_kernel<T, 8, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+          break;
+        case 4:
+          hist_rep_kernel<T, 4, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+          break;
+        case 2:
+          hist_rep_kernel<T, 2, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+          break;
+        default:
+          hist_rep_kernel<T, 1, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
+              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        }
+        return check_launch();
+      }
+    }
     if (lds && aligned16(x) && n % N == 0) {
       unsigned g = grid_for(n / N, kThreads * 8);
       hist_vec_kernel<T><<<g, kThreads, shm, stream>>>(xt, n / N, hmax, bins, skip_zeros, counts);

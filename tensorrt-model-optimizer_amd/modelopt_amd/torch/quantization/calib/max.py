@@ -39,6 +39,7 @@ class MaxCalibrator(_Calibrator):
         self._out_dtype = None
         self._last = None  # (weakref to the base of the last collected tensor, view key, _version)
         self._meta_amax = None
+        self._validated = False  # NaN/inf checks done for the current running max
 
     @property
     def amaxs(self):
@@ -77,6 +78,7 @@ class MaxCalibrator(_Calibrator):
         elif list(keep_shape) != list(self._out_shape):
             raise RuntimeError("amax shape changed!")
         quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
+        self._validated = False
         try:
             base, key = self._view_key(x)
             self._last = (weakref.ref(base), key, x._version)
@@ -102,14 +104,32 @@ class MaxCalibrator(_Calibrator):
         self._acc = None
         self._out_shape = None
         self._last = None
+        self._validated = False
 
     def validate(self):
         """The reference's per-collect asserts (calib/max.py:69-77), evaluated once."""
-        if self._acc is None:
+        if self._acc is None or self._validated:
             return
         bad = torch.stack([torch.isnan(self._acc).any(), torch.isinf(self._acc).any()]).tolist()
         assert not bad[0], "detected nan values in amax (NaN in a collected tensor)"
         assert not bad[1], "detected inf values in amax (inf in a collected tensor)"
+        self._validated = True
+
+    @staticmethod
+    def validate_many(calibrators) -> None:
+        """Batched ``validate`` for many calibrators: one concatenated NaN/inf check (one host
+        sync per device) instead of one per quantizer (448 for Llama-3-8B FP8).  Clean
+        calibrators are marked validated; if any running max holds NaN/inf, each calibrator is
+        left to raise its own AssertionError in ``compute_amax``."""
+        by_dev: dict = {}
+        for c in calibrators:
+            if isinstance(c, MaxCalibrator) and c._acc is not None and not c._validated:
+                by_dev.setdefault(c._acc.device, []).append(c)
+        for cs in by_dev.values():
+            flat = torch.cat([c._acc for c in cs])
+            if not bool((~torch.isfinite(flat)).any()):
+                for c in cs:
+                    c._validated = True
 
     def compute_amax(self):
         self.validate()

@@ -28,6 +28,7 @@ from modelopt_amd.torch.utils.distributed import DistributedProcessGroup
 from .conversion import set_quantizer_by_cfg_context
 from .nn.modules.quant_module import QuantModule
 from .nn.modules.tensor_quantizer import SequentialQuantizer, StaticBlockScaleQuantizer, TensorQuantizer
+from .utils import core_utils as quant_utils
 from .utils.names import is_quantized_linear
 
 __all__ = [
@@ -61,6 +62,12 @@ def enable_stats_collection(model: nn.Module):
 
 def finish_stats_collection(model: nn.Module, method: str | None = None, **kwargs):
     """Load amax from the calibrators, quant on, calib off (reference :1144-1167)."""
+    from .calib.max import MaxCalibrator
+
+    # one batched NaN/inf check for every max calibrator instead of a host sync per quantizer
+    MaxCalibrator.validate_many(
+        getattr(m, "_calibrator", None) for m in model.modules() if isinstance(m, TensorQuantizer)
+    )
     for _, module in model.named_modules():
         if not isinstance(module, TensorQuantizer) or module._disabled:
             continue
@@ -173,7 +180,8 @@ def max_calibrate(
     weight_only_quantize(model)
     if forward_loop is not None:
         forward_loop(model)
-    finish_stats_collection(model)
+    with quant_utils.gc_paused():
+        finish_stats_collection(model)
 
     for _, module in model.named_modules():
         if hasattr(module, "layer_sync_moe_local_experts_amax"):

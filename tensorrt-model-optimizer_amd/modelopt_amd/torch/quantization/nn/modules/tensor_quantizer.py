@@ -110,6 +110,73 @@ def _default_attribute_items() -> _AttributeItems:
     return _DEFAULT_ITEMS[0]
 
 
+# Attribute application tables (reference tensor_quantizer.py:228-290), built once instead of per
+# set_from_attribute_config call: conversion of Llama-3-8B applies ~2k attribute configs.
+_FIELDS: list = []
+_ORDER = {"num_bits": 0, "axis": 1, "unsigned": 2, "block_sizes": 3, "calibrator": 9}
+_PROPERTIES: dict = {}
+
+
+def _attribute_fields() -> frozenset:
+    if not _FIELDS:
+        _FIELDS.append(frozenset(QuantizerAttributeConfig.model_fields))
+    return _FIELDS[0]
+
+
+def _attribute_order(kv) -> int:
+    return _ORDER.get(kv[0], 5)
+
+
+def _class_properties(cls) -> frozenset:
+    props = _PROPERTIES.get(cls)
+    if props is None:
+        props = frozenset(n for k in cls.__mro__ for n, v in vars(k).items() if isinstance(v, property))
+        _PROPERTIES[cls] = props
+    return props
+
+
+def _calibrator_setter(tq, val):
+    if val in ["max", "histogram"]:
+        cls = calib.MaxCalibrator if val == "max" else calib.HistogramCalibrator
+        args, kwargs = (tq._num_bits, tq._axis, tq._unsigned), {}
+    else:
+        cls, args, kwargs = _standardize_constructor_args(val)
+    return cls(*args, **kwargs)
+
+
+def _axis_setter(tq, val):
+    if getattr(tq, "_calibrator", None) is not None:
+        tq._calibrator._axis = val
+    return val
+
+
+def _block_sizes_setter(tq, val):
+    if val is not None:
+        tq._axis = None
+        if getattr(tq, "_calibrator", None) is not None:
+            tq._calibrator._axis = None
+    return val
+
+
+def _constant_amax_setter(tq, val):
+    if val is not None:
+        tq.amax = float(val)
+    return val
+
+
+_ATTRIBUTE_SETTERS: dict[str, tuple[str, Callable]] = {
+    "enable": ("_disabled", lambda tq, v: v is False),
+    "type": ("_dynamic", lambda tq, v: v == "dynamic"),
+    "calibrator": ("_calibrator", _calibrator_setter),
+    "axis": ("_axis", _axis_setter),
+    "block_sizes": ("_block_sizes", _block_sizes_setter),
+    "backend": ("backend", lambda tq, v: v),
+    "backend_extra_args": ("backend_extra_args", lambda tq, v: v or {}),
+    "use_constant_amax": ("_use_constant_amax", lambda tq, v: v),
+    "constant_amax": ("_constant_amax", _constant_amax_setter),
+}
+
+
 class TensorQuantizer(nn.Module):
     """Tensor quantizer module (reference :136)."""
 
@@ -133,16 +200,19 @@ class TensorQuantizer(nn.Module):
             quant_attribute_cfg = _default_attribute_items()
         if amax is not None:
             self.amax = amax
-        self._use_constant_amax = False
-        self._constant_amax = None
+        d = self.__dict__  # plain values: skip nn.Module.__setattr__'s bookkeeping
+        d["_use_constant_amax"] = False
+        d["_constant_amax"] = None
         self.set_from_attribute_config(quant_attribute_cfg)
-        self._if_quant = if_quant
-        self._if_calib = if_calib
-        self._enable_pre_quant_scale = True
-        self._dequantize = False
-        self._input_dtype = None
-        self._bias_calibrator = None
-        self._quantizer_cache = None
+        d.update(
+            _if_quant=if_quant,
+            _if_calib=if_calib,
+            _enable_pre_quant_scale=True,
+            _dequantize=False,
+            _input_dtype=None,
+            _bias_calibrator=None,
+            _quantizer_cache=None,
+        )
 
     # ---- configuration --------------------------------------------------------------------
     def set_from_attribute_config(self, attribute_cfg: QuantizerAttributeConfig | dict[str, Any]):
@@ -161,52 +231,18 @@ class TensorQuantizer(nn.Module):
         else:
             items = attribute_cfg.items()
 
-        def _calibrator_setter(val):
-            if val in ["max", "histogram"]:
-                cls = calib.MaxCalibrator if val == "max" else calib.HistogramCalibrator
-                args, kwargs = (self._num_bits, self._axis, self._unsigned), {}
-            else:
-                cls, args, kwargs = _standardize_constructor_args(val)
-            return cls(*args, **kwargs)
-
-        def _axis_setter(val):
-            if getattr(self, "_calibrator", None) is not None:
-                self._calibrator._axis = val
-            return val
-
-        def _block_sizes_setter(val):
-            if val is not None:
-                self._axis = None
-                if getattr(self, "_calibrator", None) is not None:
-                    self._calibrator._axis = None
-            return val
-
-        def _constant_amax_setter(val):
-            if val is not None:
-                self.amax = float(val)
-            return val
-
-        custom: dict[str, tuple[str, Callable]] = {
-            "enable": ("_disabled", lambda v: v is False),
-            "type": ("_dynamic", lambda v: v == "dynamic"),
-            "calibrator": ("_calibrator", _calibrator_setter),
-            "axis": ("_axis", _axis_setter),
-            "block_sizes": ("_block_sizes", _block_sizes_setter),
-            "backend": ("backend", lambda v: v),
-            "backend_extra_args": ("backend_extra_args", lambda v: v or {}),
-            "use_constant_amax": ("_use_constant_amax", lambda v: v),
-            "constant_amax": ("_constant_amax", _constant_amax_setter),
-        }
+        fields = _attribute_fields()
+        custom = _ATTRIBUTE_SETTERS
         items = list(items)
         # num_bits / axis / unsigned must be set before the calibrator is constructed
-        order = {"num_bits": 0, "axis": 1, "unsigned": 2, "block_sizes": 3, "calibrator": 9}
-        items.sort(key=lambda kv: order.get(kv[0], 5))
+        items.sort(key=_attribute_order)
         for attribute, val in items:
-            assert attribute in QuantizerAttributeConfig.model_fields, (
-                f"{attribute} is not a valid `TensorQuantizer` attribute"
-            )
-            name, setter = custom.get(attribute, (f"_{attribute}", lambda v: v))
-            self._set_plain(name, setter(val))
+            assert attribute in fields, f"{attribute} is not a valid `TensorQuantizer` attribute"
+            spec = custom.get(attribute)
+            if spec is None:
+                self._set_plain("_" + attribute, val)
+            else:
+                self._set_plain(spec[0], spec[1](self, val))
         if self._rotate_enabled():
             raise NotImplementedError("modelopt_amd: input rotation (QuaRot/SpinQuant) is out of scope")
         if getattr(self, "_bias", None):
@@ -223,7 +259,7 @@ class TensorQuantizer(nn.Module):
             or name in d["_parameters"]
             or name in d["_buffers"]
             or name in d["_modules"]
-            or isinstance(getattr(type(self), name, None), property)
+            or name in _class_properties(type(self))
         ):
             setattr(self, name, value)
         else:

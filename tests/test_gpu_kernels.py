@@ -277,6 +277,39 @@ def test_reduce_amax(gpu, dtype, shape, axis):
     assert same_bits(out, ref), mismatch(out, ref)
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize(
+    "shape,axis",
+    [
+        ((5000, 4104), -1),  # columns: a partial last 64-vector chunk
+        ((3000, 96), -1),  # columns: fewer than 64 vectors across (many row lanes)
+        ((70000, 64), -1),  # columns: long and narrow (slab count capped by rows)
+        ((1001, 128), 0),  # short rows: R not a multiple of the rows per block
+        ((37, 14344), 0),  # long rows: several chunks per row, partial last chunk
+        ((6, 5, 40), (0, 2)),  # short rows with P > 1 (atomic fold onto r % K)
+    ],
+)
+def test_reduce_amax_launch_shapes(gpu, dtype, shape, axis):
+    """Edge shapes of the wide-column, unrolled-row and short-row amax launches."""
+    from modelopt_amd.torch.quantization.utils.core_utils import reduce_amax
+
+    g = torch.Generator().manual_seed(sum(shape))
+    x = (torch.randn(shape, generator=g) * 3).to(dtype)
+    x.view(-1)[:: 997] *= 50  # scattered outliers
+    raxis = R.convert_quantization_axis_to_reduce_axis(x, axis)
+    ref = R.reduce_amax(x, axis=raxis)
+    out = reduce_amax(x.to(gpu), axis=raxis)
+    assert same_bits(out, ref), mismatch(out, ref)
+    # accumulation into an existing running max (the calibrator's fold), twice the same input
+    from modelopt_amd.torch.quantization.utils.core_utils import reduce_amax_accumulate
+
+    acc = torch.zeros(ref.numel(), dtype=torch.float32, device=gpu)
+    xg = x.to(gpu)
+    reduce_amax_accumulate(xg, acc, raxis)
+    reduce_amax_accumulate(xg * 0.5, acc, raxis)
+    assert torch.equal(acc.cpu(), ref.float().reshape(-1))
+
+
 def test_reduce_amax_nan_inf(gpu):
     from modelopt_amd.torch.quantization.utils.core_utils import reduce_amax
 
@@ -304,6 +337,30 @@ def test_histogram_matches_histc(gpu, bins, dtype):
     ref = torch.histc(xa, bins=bins, min=0, max=float(hmax))
     counts = torch.zeros(bins, dtype=torch.int32, device=gpu)
     ops().histogram_abs_accumulate(x.to(gpu), hmax.to(gpu).float(), counts, bins, False)
+    assert torch.equal(counts.cpu().float(), ref), (counts.cpu().float() - ref).abs().max()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("bins", [64, 2048, 4096, 9000])
+@pytest.mark.parametrize("skip_zeros", [False, True])
+def test_histogram_16bit_table_path(gpu, dtype, bins, skip_zeros):
+    """The per-block bin table of the 16-bit path: zeros, values at / above the range end,
+    NaN / inf, subnormals, every bin-count regime (REP 8 / 4 / 2 / 1)."""
+    g = torch.Generator().manual_seed(bins + skip_zeros)
+    x = (torch.randn(1 << 17, generator=g) * 2).to(dtype)
+    x[:500] = 0
+    x[500:510] = float("nan")
+    x[510:520] = float("inf")
+    x[520:600] = torch.finfo(dtype).tiny / 4  # subnormals
+    hmax = x[600:].float().abs().max() * 0.9  # some finite values lie above the range
+    x[600:610] = hmax.to(dtype)
+    xa = x.float().abs()
+    keep = ~torch.isnan(xa) & (xa <= hmax)
+    if skip_zeros:
+        keep &= xa != 0
+    ref = torch.histc(xa[keep], bins=bins, min=0, max=float(hmax))
+    counts = torch.zeros(bins, dtype=torch.int32, device=gpu)
+    ops().histogram_abs_accumulate(x.to(gpu), hmax.to(gpu).float(), counts, bins, skip_zeros)
     assert torch.equal(counts.cpu().float(), ref), (counts.cpu().float() - ref).abs().max()
 
 
