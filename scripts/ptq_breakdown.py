@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--config", default="FP8_DEFAULT_CFG")
-    ap.add_argument("--trace", default=None, help="write a torch.profiler chrome trace of one calib batch")
+    ap.add_argument("--trace", default=None, help="write a torch.profiler chrome trace of one fake-quant batch")
+    ap.add_argument("--calib-trace", action="store_true", help="print kernel totals of two calibration batches")
     a = ap.parse_args()
 
     import modelopt_amd.torch.quantization as mtq
@@ -102,6 +103,15 @@ def main():
         res["calib_enqueue_one_batch_s"] = time.perf_counter() - t0
         torch.cuda.synchronize()
         res["calib_forward_s"], _ = timed(lambda: forward_loop(model))
+        if a.calib_trace:
+            from torch.profiler import ProfilerActivity, profile
+
+            with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+                with torch.no_grad():
+                    for b in batches[:2]:
+                        model(b)
+                torch.cuda.synchronize()
+            print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=30), file=sys.stderr)
     finally:
         TensorQuantizer.forward = orig
     res["quantizer_calls"] = calls[0]

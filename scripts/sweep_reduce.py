@@ -65,7 +65,7 @@ print(json.dumps(out))
 VARIANTS = {
     "cols": ("MTQ_AMD_COLS_VARIANT", {0: "wide auto", 1: "old per-lane slab", 5: "wide 1/CU", 3: "wide 2/CU", 4: "wide 0.5/CU"}),
     "rows": ("MTQ_AMD_ROWS_VARIANT", {0: "unrolled U=8 / short RU=4 (new)", 1: "old"}),
-    "hist": ("MTQ_AMD_HIST_VARIANT", {0: "16-bit LUT rep8", 7: "16-bit LUT rep4", 1: "old", 3: "rep4 4/CU"}),
+    "hist": ("MTQ_AMD_HIST_VARIANT", {0: "div rep4 2/CU", 8: "div rep8 1/CU", 9: "div rep8 2/CU", 1: "old"}),
 }
 
 res = {}

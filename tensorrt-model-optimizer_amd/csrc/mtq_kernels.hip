@@ -1186,16 +1186,17 @@ __global__ __launch_bounds__(kThreads) void hist_vec_kernel(const T *__restrict_
     if (sh[b]) atomicAdd(counts + b, sh[b]);
 }
 
-// Replicated-LDS form: REP copies of the bins, interleaved (bin b, copy c at b*REP + c) and
-// picked by lane, so lanes of one ds_add that land in the same bin -- calibration data piles
-// into the first few dozen of 2048 bins -- hit REP different words instead of serialising on one.
-// Each block owns one contiguous chunk of vectors with U loads in flight per lane; blocks are
-// few (O(CUs)) so the flush (one global atomic per non-zero bin per block) stays cheap.
+// Division form (default, any dtype): the per-element true division of the formula above is
+// replaced by Markstein's correction q = fma(fma(-q0, span, t), y, q0), q0 = t * y,
+// y = RN(1 / span), which is the correctly rounded t / span for normal operands (checked on
+// the host against the IEEE division for every bf16 and f16 |x| at 20 000 random ranges and
+// bin counts: 6.96e8 cases, no difference; scripts/check_hist_division.c).  4 VALU ops instead
+// of the ~10 of a divide, no table read: one LDS add per element into REP interleaved copies.
+constexpr int kHistDivThreads = 1024;
 template <typename T, int REP, int U>
-__global__ __launch_bounds__(kThreads) void hist_rep_kernel(const T *__restrict__ x, int64_t nvec,
-                                                             int64_t vec_per_block,
-                                                             const float *hmax, int bins,
-                                                             int skip_zeros, uint32_t *counts) {
+__global__ __launch_bounds__(kHistDivThreads) void hist_div_kernel(
+    const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
+    int skip_zeros, uint32_t *counts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
   using V = Vec<T>;
   float lo = 0.f, hi = *hmax;
@@ -1205,94 +1206,19 @@ __global__ __launch_bounds__(kThreads) void hist_rep_kernel(const T *__restrict_
   }
   const float fb = (float)bins;
   const float span = hi - lo;
-  for (int b = threadIdx.x; b < bins * REP; b += kThreads) sh[b] = 0;
+  const float y = 1.f / span;
+  const uint32_t last = (uint32_t)bins - 1u;
+  for (int b = threadIdx.x; b < bins * REP; b += kHistDivThreads) sh[b] = 0;
   __syncthreads();
   const int c = threadIdx.x % REP;
   const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
   int64_t v1 = v0 + vec_per_block;
   v1 = v1 < nvec ? v1 : nvec;
-  for (int64_t i = v0 + threadIdx.x; i < v1; i += (int64_t)kThreads * U) {
+  for (int64_t i = v0 + threadIdx.x; i < v1; i += (int64_t)kHistDivThreads * U) {
     V v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t k = i + (int64_t)u * kThreads;
-      if (k < v1)
-        v[u] = ldg_vec_nt(x + k * V::N);
-      else
-        v[u].raw = make_uint4(0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (i + (int64_t)u * kThreads >= v1) continue;
-#pragma unroll
-      for (int j = 0; j < V::N; ++j) {
-        float a = fabsf(Elem<T>::ld(v[u].e[j]));
-        bool ok = (a >= lo && a <= hi) && !(skip_zeros && a == 0.f);
-        if (ok) {
-          int b = (int)(((a - lo) * fb) / span);
-          if (b == bins) b -= 1;
-          atomicAdd(sh + b * REP + c, 1u);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < bins; b += kThreads) {
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < REP; ++k) s += sh[b * REP + k];
-    if (s) atomicAdd(counts + b, s);
-  }
-}
-
-// 16-bit inputs (bf16 / f16): |x| has only 2^15 bit patterns, so each block first tabulates the
-// bin of every pattern in LDS (uint16, 0xFFFF = dropped) with exactly the per-element formula
-// above (fp32 multiply, true division, truncation, last-bin clamp, range / NaN / zero checks),
-// then the stream costs a mask, one LDS table read and one LDS add per element instead of ~25
-// VALU operations (the divide dominates) -- the VALU-bound kernels above reach ~2.4 TB/s.
-// Patterns above hi are dropped without a division, so the table costs ~1-3 us per block.
-// One 1024-thread block per CU (64 KB table + up to 64 KB of bins in LDS).
-constexpr int kHistLutThreads = 1024;
-constexpr int kHistLutWords = 16384;
-template <typename T, int REP, int U>
-__global__ __launch_bounds__(kHistLutThreads) void hist_lut_kernel(
-    const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
-    int skip_zeros, uint32_t *counts) {
-  static_assert(sizeof(T) == 2, "16-bit element types only");
-  __shared__ uint16_t lut[32768];
-  __shared__ uint32_t sh[kHistLutWords];
-  using V = Vec<T>;
-  float lo = 0.f, hi = *hmax;
-  if (hi == lo) {
-    lo -= 1.f;
-    hi += 1.f;
-  }
-  const float fb = (float)bins;
-  const float span = hi - lo;
-  for (int b = threadIdx.x; b < bins * REP; b += kHistLutThreads) sh[b] = 0;
-  for (int m = threadIdx.x; m < 32768; m += kHistLutThreads) {
-    T t;
-    uint16_t bits = (uint16_t)m;
-    memcpy(&t, &bits, 2);
-    const float a = Elem<T>::ld(t);
-    uint16_t e = 0xFFFF;
-    if ((a >= lo && a <= hi) && !(skip_zeros && a == 0.f)) {
-      int b = (int)(((a - lo) * fb) / span);
-      if (b == bins) b -= 1;
-      e = (uint16_t)b;
-    }
-    lut[m] = e;
-  }
-  __syncthreads();
-  const int c = threadIdx.x % REP;
-  const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
-  int64_t v1 = v0 + vec_per_block;
-  v1 = v1 < nvec ? v1 : nvec;
-  for (int64_t i = v0 + threadIdx.x; i < v1; i += (int64_t)kHistLutThreads * U) {
-    V v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t k = i + (int64_t)u * kHistLutThreads;
+      const int64_t k = i + (int64_t)u * kHistDivThreads;
       if (k < v1)
         v[u] = ldg_vec_nt(x + k * V::N);
       else
@@ -1300,17 +1226,23 @@ __global__ __launch_bounds__(kHistLutThreads) void hist_lut_kernel(
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t w[4] = {v[u].raw.x, v[u].raw.y, v[u].raw.z, v[u].raw.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t m = (w[j >> 1] >> ((j & 1) * 16)) & 0x7fffu;
-        const uint32_t b = lut[m];
-        if (b != 0xFFFFu) atomicAdd(sh + b * REP + c, 1u);
+      for (int j = 0; j < V::N; ++j) {
+        const float a = fabsf(Elem<T>::ld(v[u].e[j]));
+        // a >= 0 >= lo always; NaN fails the compare
+        if (a <= hi && !(skip_zeros && a == 0.f)) {
+          const float t = (a - lo) * fb;
+          const float q0 = t * y;
+          const float q = __builtin_fmaf(__builtin_fmaf(-q0, span, t), y, q0);
+          uint32_t b = (uint32_t)(int)q;
+          b = b < last ? b : last;  // q == bins -> last bin (histc); overflow guard
+          atomicAdd(sh + b * REP + c, 1u);
+        }
       }
     }
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < bins; b += kHistLutThreads) {
+  for (int b = threadIdx.x; b < bins; b += kHistDivThreads) {
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < REP; ++k) s += sh[b * REP + k];
@@ -2031,70 +1963,38 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
     const size_t shm = lds ? (size_t)bins * 4 : 0;
     static int hv = -1;
     const int var = env_variant("MTQ_AMD_HIST_VARIANT", &hv);
-    if constexpr (sizeof(T) == 2) {
-      if ((var == 0 || var == 6 || var == 7) && aligned16(x) && n % N == 0 && bins <= kHistLutWords) {
-        int rep = var == 6 ? 1 : var == 7 ? 4 : 8;
-        while (rep > 1 && bins * rep > kHistLutWords) rep >>= 1;
-        const int64_t nvec = n / N;
-        int64_t blocks = num_cus();
-        const int64_t min_per_block = (int64_t)kHistLutThreads * 8;
-        int64_t vpb = (nvec + blocks - 1) / blocks;
-        vpb = vpb < min_per_block ? min_per_block : vpb;
-        blocks = (nvec + vpb - 1) / vpb;
-        switch (rep) {
-        case 8:
-          hist_lut_kernel<T, 8, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-          break;
-        case 4:
-          hist_lut_kernel<T, 4, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-          break;
-        case 2:
-          hist_lut_kernel<T, 2, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-          break;
-        default:
-          hist_lut_kernel<T, 1, 4><<<(unsigned)blocks, kHistLutThreads, 0, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-        }
-        return check_launch();
+    // variants (MTQ_AMD_HIST_VARIANT, scripts/sweep_reduce.py): 0 = REP 4, 2 blocks per CU
+    // (4.3 TB/s on bf16 [32768, 4096]); 8 = REP 8, 1 block per CU; 9 = REP 8, 2 per CU;
+    // 1 = the plain LDS-privatised kernels below (2.4 TB/s, VALU-bound on the division)
+    if ((var == 0 || var == 8 || var == 9) && aligned16(x) && n % N == 0 && bins <= 16384) {
+      int rep = var == 0 ? 4 : 8;
+      while (rep > 1 && (int64_t)bins * rep > 16384) rep >>= 1;
+      const int per_cu = var == 8 ? 1 : 2;
+      const int64_t nvec = n / N;
+      int64_t blocks = (int64_t)num_cus() * per_cu;
+      const int64_t min_per_block = (int64_t)kHistDivThreads * 8;
+      int64_t vpb = (nvec + blocks - 1) / blocks;
+      vpb = vpb < min_per_block ? min_per_block : vpb;
+      blocks = (nvec + vpb - 1) / vpb;
+      const size_t shr = (size_t)bins * rep * 4;
+      switch (rep) {
+      case 8:
+        hist_div_kernel<T, 8, 4><<<(unsigned)blocks, kHistDivThreads, shr, stream>>>(
+            xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        break;
+      case 4:
+        hist_div_kernel<T, 4, 4><<<(unsigned)blocks, kHistDivThreads, shr, stream>>>(
+            xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        break;
+      case 2:
+        hist_div_kernel<T, 2, 4><<<(unsigned)blocks, kHistDivThreads, shr, stream>>>(
+            xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        break;
+      default:
+        hist_div_kernel<T, 1, 4><<<(unsigned)blocks, kHistDivThreads, shr, stream>>>(
+            xt, nvec, vpb, hmax, bins, skip_zeros, counts);
       }
-    }
-    if (var != 1 && aligned16(x) && n % N == 0) {
-      // replicated-LDS form: (REP, blocks per CU) by variant; REP * bins words must fit 64 KB
-      int rep = 4, per_cu = 4;
-      if (var == 2) rep = 1;
-      if (var == 4) rep = 8, per_cu = 2;
-      if (var == 5) per_cu = 8;
-      while (rep > 1 && (int64_t)bins * rep * 4 > 65536) rep >>= 1;
-      if ((int64_t)bins * rep * 4 <= 65536) {
-        const int64_t nvec = n / N;
-        int64_t blocks = (int64_t)num_cus() * per_cu;
-        const int64_t min_per_block = (int64_t)kThreads * 4;
-        int64_t vpb = (nvec + blocks - 1) / blocks;
-        vpb = vpb < min_per_block ? min_per_block : vpb;
-        blocks = (nvec + vpb - 1) / vpb;
-        const size_t shr = (size_t)bins * rep * 4;
-        switch (rep) {
-        case 8:
-          hist_rep_kernel<T, 8, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-          break;
-        case 4:
-          hist_rep_kernel<T, 4, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-          break;
-        case 2:
-          hist_rep_kernel<T, 2, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-          break;
-        default:
-          hist_rep_kernel<T, 1, 4><<<(unsigned)blocks, kThreads, shr, stream>>>(
-              xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-        }
-        return check_launch();
-      }
+      return check_launch();
     }
     if (lds && aligned16(x) && n % N == 0) {
       unsigned g = grid_for(n / N, kThreads * 8);

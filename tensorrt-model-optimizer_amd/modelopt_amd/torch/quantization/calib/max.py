@@ -25,6 +25,10 @@ from .calibrator import _Calibrator
 
 __all__ = ["MaxCalibrator"]
 
+# The last tensor reduced by a calibrator: (weakref to its base, (view key, _version, reduce
+# axes), weakref to the calibrator, its per-call amax buffer or None).  See _accumulate.
+_SHARED = None
+
 
 class MaxCalibrator(_Calibrator):
     """Tracks the absolute max of all collected tensors (per-tensor or along ``axis``)."""
@@ -40,6 +44,8 @@ class MaxCalibrator(_Calibrator):
         self._last = None  # (weakref to the base of the last collected tensor, view key, _version)
         self._meta_amax = None
         self._validated = False  # NaN/inf checks done for the current running max
+        self._share = False  # another calibrator collects the same tensors: publish results
+        self._tmp = None
 
     @property
     def amaxs(self):
@@ -77,15 +83,51 @@ class MaxCalibrator(_Calibrator):
                 self._out_dtype = torch.get_default_dtype()
         elif list(keep_shape) != list(self._out_shape):
             raise RuntimeError("amax shape changed!")
-        quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
         self._validated = False
         try:
             base, key = self._view_key(x)
             self._last = (weakref.ref(base), key, x._version)
         except TypeError:
+            base = None
             self._last = None
+        self._accumulate(x, reduce_axis, base)
         if self._track_amax:
             self._amaxs.append(quant_utils.reduce_amax(x, axis=reduce_axis).cpu().numpy())
+
+    def _accumulate(self, x, reduce_axis, base):
+        """Fold max|x| into the running max, sharing one reduction between calibrators that
+        collect the very same tensor: q/k/v_proj (and gate/up_proj) input quantizers all see
+        the one normalised hidden state, so the reference reduces it 3 (2) times per layer and
+        batch.  The first calibrator to see a tensor records it; a sibling that then sees the
+        same tensor marks the first one as a *producer*, which from the next batch on reduces
+        into a private buffer that the siblings fold in with one elementwise max.  max is exact
+        and order-free, so every running max is bit-identical to an unshared collect."""
+        global _SHARED
+        if base is None or self._track_amax:
+            quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
+            return
+        key = (self._last[1], x._version, None if reduce_axis is None else tuple(reduce_axis))
+        entry = _SHARED
+        if entry is not None and entry[0]() is base and entry[1] == key and entry[2]() is not self:
+            result = entry[3]
+            if result is not None and result.numel() == self._acc.numel():
+                torch.maximum(self._acc, result, out=self._acc)
+                return
+            producer = entry[2]()
+            if producer is not None:
+                producer._share = True
+            quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
+            return
+        if getattr(self, "_share", False):
+            if self._tmp is None or self._tmp.numel() != self._acc.numel():
+                self._tmp = torch.empty_like(self._acc)
+            self._tmp.zero_()
+            quant_utils.reduce_amax_accumulate(x, self._tmp, reduce_axis)
+            torch.maximum(self._acc, self._tmp, out=self._acc)
+            _SHARED = (weakref.ref(base), key, weakref.ref(self), self._tmp)
+        else:
+            quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
+            _SHARED = (weakref.ref(base), key, weakref.ref(self), None)
 
     def _result(self):
         if self._acc is None:
@@ -101,10 +143,14 @@ class MaxCalibrator(_Calibrator):
         return self._result()
 
     def reset(self):
+        global _SHARED
         self._acc = None
         self._out_shape = None
         self._last = None
         self._validated = False
+        self._tmp = None
+        if _SHARED is not None and _SHARED[2]() is self:
+            _SHARED = None
 
     def validate(self):
         """The reference's per-collect asserts (calib/max.py:69-77), evaluated once."""

@@ -195,3 +195,35 @@ def test_weight_collect_once_per_version(gpu):
         w.mul_(2)
     c.collect(w)
     assert torch.equal(c.compute_amax(), a0 * 2)
+
+
+@pytest.mark.parametrize("axis", [None, -1])
+def test_shared_input_collect_matches_independent(gpu, axis):
+    """Calibrators that collect the very same tensor (q/k/v_proj input quantizers) share one
+    reduction from the second batch on; every running max must equal an unshared collect,
+    including when the shared tensor is modified in place between siblings (NaN included)."""
+    from modelopt_amd.torch.quantization.calib import MaxCalibrator
+    from oracle import ref_ops as R
+
+    cs = [MaxCalibrator(axis=axis) for _ in range(3)]
+    lone = MaxCalibrator(axis=axis)
+    g = torch.Generator().manual_seed(7)
+    seen = [[] for _ in range(3)]
+    for step in range(5):
+        x = (torch.randn(64, 256, generator=g) * (step + 1)).to(torch.bfloat16).to(gpu)
+        for i, c in enumerate(cs):
+            if step == 3 and i == 2:
+                x.mul_(3)  # in place between siblings: the third must reduce it again
+            if step == 4 and i == 1:
+                x[5, 7] = float("nan")
+            c.collect(x)
+            seen[i].append(x.clone().cpu())
+        lone.collect(torch.randn(64, 256, device=gpu).to(torch.bfloat16))  # interleaved other tensor
+    assert cs[0]._share  # the first calibrator became the producer
+    raxis = None if axis is None else [0]
+    for i, c in enumerate(cs):
+        want = torch.stack([R.reduce_amax(t, axis=raxis).float().reshape(-1) for t in seen[i]]).amax(0)
+        got = c._acc.cpu()
+        assert torch.equal(torch.isnan(got), torch.isnan(want)), i
+        ok = ~torch.isnan(want)
+        assert torch.equal(got[ok], want[ok]), i
