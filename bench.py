@@ -317,7 +317,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "mtq fp8 axis (Fp8AxisVecOp<bf16>) via modelopt_amd::quantize_op",
+            "kernel": "ew_group_kernel<bf16, Fp8AxisVecOp, U=2> via modelopt_amd::quantize_op",
             "algorithmic_bytes_per_launch": alg_bytes,
             "mean_launch_ms": round(ms, 4),
         },

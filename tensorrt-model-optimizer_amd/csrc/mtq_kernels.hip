@@ -196,11 +196,14 @@ template <typename T> struct IntAxisVecOp {
     }
     return (vi / inner_vec64) % axis64;
   }
-  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) {
-    IntQ q = make_intq(load_as_float(amax, amax_dtype, chan(vi)), max_bound, min_bound);
+  __device__ __forceinline__ IntQ qparam(int64_t vi) const {
+    return make_intq(load_as_float(amax, amax_dtype, chan(vi)), max_bound, min_bound);
+  }
+  __device__ __forceinline__ static void apply(Vec<T> &v, const IntQ &q) {
 #pragma unroll
     for (int j = 0; j < Vec<T>::N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
   }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) { apply(v, qparam(vi)); }
   __device__ __forceinline__ float one(float x, int64_t i) {
     int64_t c = (i / (inner_vec64 * Vec<T>::N)) % axis64;
     return int_qdq(x, make_intq(load_as_float(amax, amax_dtype, c), max_bound, min_bound));
@@ -269,9 +272,11 @@ template <typename T> struct Fp8AxisVecOp {
     }
     return (vi / inner_vec64) % axis64;
   }
-  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) {
-    fp8_vec(v, make_fp8q(load_as_float(amax, amax_dtype, chan(vi))));
+  __device__ __forceinline__ Fp8Q qparam(int64_t vi) const {
+    return make_fp8q(load_as_float(amax, amax_dtype, chan(vi)));
   }
+  __device__ __forceinline__ static void apply(Vec<T> &v, const Fp8Q &q) { fp8_vec(v, q); }
+  __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) { fp8_vec(v, qparam(vi)); }
   __device__ __forceinline__ float one(float x, int64_t i) {
     int64_t c = (i / (inner_vec64 * Vec<T>::N)) % axis64;
     return fp8_one(x, make_fp8q(load_as_float(amax, amax_dtype, c)));
@@ -316,6 +321,51 @@ template <typename T> struct Fp8CastOp {
 };
 
 // --------------------------------------------------------------------------------------------
+// Block-grouped form of the axis ops for short channels (the static block view: one amax per
+// `inner` = VB vectors, e.g. 16 bf16 vectors for block 128).  A lane takes U vectors of the SAME
+// channel, so the per-channel parameters -- an amax load and two correctly rounded divisions for
+// FP8 (make_fp8q), one for INT -- are paid once per U vectors instead of per vector.  The LPB =
+// VB / U lanes of a channel read consecutive 16-byte vectors, so each load instruction still
+// covers whole aligned 128-byte lines (LPB >= 8).  Each wave covers 64 * U vectors = 64 / LPB
+// channels; one contiguous chunk of 256 * U vectors per block, non-temporal, as ew_vec_kernel.
+// --------------------------------------------------------------------------------------------
+template <typename T, class Op, int U>
+__global__ __launch_bounds__(kThreads) void ew_group_kernel(const T *__restrict__ x,
+                                                             T *__restrict__ y, int64_t nvec,
+                                                             int lpb, Op op) {
+  using V = Vec<T>;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t wb = ((int64_t)blockIdx.x * kThreads + (int64_t)w * 64) * U;
+  const int k = lane / lpb, pos = lane - k * lpb;
+  const int64_t v0 = wb + (int64_t)k * lpb * U + pos;  // first vector of this lane
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = v0 + (int64_t)u * lpb;
+    if (i < nvec) v[u] = ldg_vec_nt(x + i * V::N);
+  }
+  if (v0 >= nvec) return;
+  const auto q = op.qparam(v0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = v0 + (int64_t)u * lpb;
+    if (i < nvec) {
+      Op::apply(v[u], q);
+      stg_vec_nt(y + i * V::N, v[u]);
+    }
+  }
+}
+
+int group_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("MTQ_AMD_GROUP_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+// --------------------------------------------------------------------------------------------
 // Axis dispatch shared by INT and FP8
 // --------------------------------------------------------------------------------------------
 template <typename T, template <typename> class VecOp, template <typename> class ElemOp,
@@ -332,6 +382,26 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
     if (op.small) {
       op.inner_vec = make_fastdiv((uint32_t)op.inner_vec64);
       op.axis = make_fastdiv((uint32_t)axis_size);
+    }
+    // short channels of whole vectors (static block quant): the grouped kernel, U = 2, when a
+    // channel spans 16..64 vectors (LPB = 8..32 lanes) and the buffers are 16-byte aligned;
+    // the vector tail n % N goes through the scalar kernel as in launch_ew.
+    const int64_t vb = op.inner_vec64;
+    const int gv = group_variant();
+    if (gv != 1 && vb >= 16 && vb <= 64 && (vb & (vb - 1)) == 0 && aligned16(x) && aligned16(y)) {
+      constexpr int U = 2;
+      const int64_t nvec = n / N;
+      const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
+      if (nvec > 0)
+        ew_group_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec, (int)(vb / U), op);
+      const int64_t done = nvec * N;
+      if (done < n) {
+        unsigned gs = grid_for(n - done, kThreads);
+        ew_scalar_kernel<T, VecOp<T>><<<gs, kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), done, n, op);
+      }
+      return check_launch();
     }
     return launch_ew<T>(x, y, n, op, stream);
   }
