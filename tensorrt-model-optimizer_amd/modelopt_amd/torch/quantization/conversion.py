@@ -48,11 +48,31 @@ def quantizer_state(model: nn.Module) -> dict[str, Any]:
 
 
 def restore_quantizer_state(model: nn.Module, config, metadata: dict):
-    """Restore quantizer properties + buffer shapes from ``metadata["quantizer_state"]``."""
+    """Restore quantizer properties + buffer shapes from ``metadata["quantizer_state"]``
+    (reference :125-168): the saved and the model's quantizer sets must match; static-block
+    quantizers are promoted before their state is applied (:103-108)."""
+    from .nn.modules.tensor_quantizer import StaticBlockScaleQuantizer
+
+    if "quantizer_state" not in metadata:
+        return model
     state = metadata["quantizer_state"]
+    current = quantizer_state(model).keys()
+    unmatched, extra = state.keys() - current, current - state.keys()
+    if unmatched:
+        raise RuntimeError(f"Unmatched keys in quantizer state_dict: {unmatched}")
+    if extra:
+        raise RuntimeError(f"Extra keys in quantizer state_dict: {extra}")
     for name, module in model.named_modules():
         if isinstance(module, TensorQuantizer) and name in state:
-            module.set_from_modelopt_state(state[name])
+            st = state[name]
+            if (st.get("_is_static_block_scale_quantizer") or st.get("_is_nvfp4_static_quantizer")) and not isinstance(
+                module, StaticBlockScaleQuantizer
+            ):
+                StaticBlockScaleQuantizer.from_tensor_quantizer(module)
+            module.set_from_modelopt_state(st)
+    for name, module in model.named_modules():
+        if isinstance(module, QuantModule):
+            module.modelopt_post_restore(name)
     return model
 
 

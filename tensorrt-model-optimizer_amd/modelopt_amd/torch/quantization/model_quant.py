@@ -134,6 +134,7 @@ def quantize(model: nn.Module, config: dict[str, Any] | QuantizeConfig, forward_
         config = QuantizeConfig(**config)
     from .conversion import replace_quant_module, set_quantizer_by_cfg
 
+    model.__dict__["_modelopt_amd_mode"] = {"config": config.model_dump()}  # for mto.modelopt_state
     with _gc_paused():
         if not is_quantized(model):
             # convert_to_quantized_model minus its metadata dict: calibrate() records the state once

@@ -24,15 +24,22 @@ class _QuantLinear(QuantLinearConvBase):
 
 
 class QuantLinear(nn.Linear):
-    """``nn.Linear`` that is born quantized (legacy constructor form, reference :56-61)."""
+    """``nn.Linear`` that is born quantized (legacy constructor form, reference :56-61).  The
+    class-level ``default_quant_desc_input`` / ``default_quant_desc_weight`` apply when no
+    descriptor is passed (reference tests/unit/torch/quantization/test_quant_linear.py:199-222)."""
+
+    default_quant_desc_input = tensor_quant.QUANT_DESC_8BIT_PER_TENSOR
+    default_quant_desc_weight = tensor_quant.QUANT_DESC_8BIT_LINEAR_WEIGHT_PER_ROW
 
     def __new__(cls, *args, quant_desc_input=None, quant_desc_weight=None, **kwargs):
         m = nn.Linear(*args, **kwargs)
         QuantModuleRegistry.convert(m)
-        if quant_desc_input is not None:
-            m.input_quantizer.set_from_attribute_config(quant_desc_input)
-        if quant_desc_weight is not None:
-            m.weight_quantizer.set_from_attribute_config(quant_desc_weight)
+        m.input_quantizer.set_from_attribute_config(
+            cls.default_quant_desc_input if quant_desc_input is None else quant_desc_input
+        )
+        m.weight_quantizer.set_from_attribute_config(
+            cls.default_quant_desc_weight if quant_desc_weight is None else quant_desc_weight
+        )
         return m
 
 

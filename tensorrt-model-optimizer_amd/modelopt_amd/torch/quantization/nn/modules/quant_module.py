@@ -12,6 +12,7 @@ to ``type("Quant" + cls, (quant_cls, cls))`` (parameters and buffers untouched) 
 from __future__ import annotations
 
 import contextlib
+import warnings
 from typing import Any
 
 import torch
@@ -157,6 +158,26 @@ class QuantModule(nn.Module):
                     weight = getattr(self, weight_name, None)
                 if isinstance(weight, torch.Tensor):
                     self._fold_weight_quantizer(attr, (weight,), keep_attrs)
+
+    def modelopt_post_restore(self, prefix: str = ""):
+        """Move restored quantizer buffers to the device of the module's own parameters
+        (reference quant_module.py:92-121): restored buffers are created on the CPU."""
+        device = None
+        for name, t in self.state_dict().items():
+            parent = self.get_submodule(name.rsplit(".", 1)[0]) if "." in name else self
+            if not isinstance(parent, TensorQuantizer):
+                device = t.device
+                break
+        if device is None:
+            warnings.warn(
+                f"Could not identify the device for TensorQuantizer states of {prefix}. "
+                "Please move the model to the right device now. This can be done by calling "
+                "`model.to(device)`."
+            )
+            return
+        for module in self.modules():
+            if isinstance(module, TensorQuantizer):
+                module.to(device)
 
     def export(self) -> nn.Module:
         """Drop the quantizers and restore the original class (the DynamicModule 'export')."""

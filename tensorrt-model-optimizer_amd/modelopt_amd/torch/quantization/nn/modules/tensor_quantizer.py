@@ -22,7 +22,7 @@ import copy
 import math
 import warnings
 from collections.abc import Callable
-from typing import Any
+from typing import Any, Protocol
 
 import torch
 import torch.nn.functional as F
@@ -44,6 +44,7 @@ __all__ = [
     "SequentialQuantizer",
     "StaticBlockScaleQuantizer",
     "TensorQuantizer",
+    "TensorQuantizerCache",
     "is_registered_quant_backend",
     "register_quant_backend",
     "unregister_quant_backend",
@@ -72,6 +73,11 @@ def unregister_quant_backend(name: str) -> None:
 
 def is_registered_quant_backend(name: str) -> bool:
     return name in _QUANT_FUNCTIONAL_BACKENDS
+
+
+class TensorQuantizerCache(Protocol):
+    """Per-quantizer cache a custom backend may keep in ``TensorQuantizer._quantizer_cache``
+    (reference tensor_quantizer.py:132-133); never saved in the modelopt state."""
 
 
 def _standardize_constructor_args(val):
