@@ -54,6 +54,8 @@ class HistogramCalibrator(_Calibrator):
 
     @torch.no_grad()
     def collect(self, x):
+        if x.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+            x = x.float()  # the reference histograms x.float() (histogram.py:82); exact for ints
         # max|x| (equals the reference's max over the non-zero |x| when skip_zeros, histogram.py:105-112)
         x_max = torch.zeros((), dtype=torch.float32, device=x.device)
         quant_utils.reduce_amax_accumulate(x, x_max, None)

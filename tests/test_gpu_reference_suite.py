@@ -1249,3 +1249,169 @@ def test_legacy_dict_format_end_to_end(mtq, tq_mod):
                 assert module.is_enabled and module.num_bits == 8
             elif name.endswith("output_quantizer"):
                 assert not module.is_enabled
+
+
+# ------------------------------------------------------------------------------------------------
+# unit/torch/quantization/test_calibrator.py:28-354 (Max / Histogram / Entropy / MSE / Percentile
+# calibrators) on device tensors; amax values also checked against the oracle's calibrators
+# (oracle/ref_ops.py, the reference's histogram.py restated on the CPU).
+# ------------------------------------------------------------------------------------------------
+def _calib(gpu):
+    from modelopt_amd.torch.quantization import calib
+
+    return calib
+
+
+class TestMaxCalibrator:
+    def test_simple_run(self, gpu):
+        c = _calib(gpu).MaxCalibrator(8, None, False)
+        x1, x2 = torch.rand(16).cuda(), torch.rand(16).cuda()
+        c.collect(x1)
+        c.collect(x2)
+        assert torch.equal(c.compute_amax(), torch.max(x1.max(), x2.max()))
+        _calib(gpu).MaxCalibrator(8, None, True)
+
+    @pytest.mark.parametrize("axis", [0, -4])
+    def test_fine_grain(self, gpu, axis):
+        from modelopt_amd.torch.quantization.utils import core_utils as quant_utils
+
+        c = _calib(gpu).MaxCalibrator(8, axis, False)
+        x1, x2 = torch.rand(3, 4, 2, 2).cuda(), torch.rand(3, 4, 2, 2).cuda()
+        c.collect(x1)
+        c.collect(x2)
+        assert c.compute_amax().shape[0] == 3
+        assert torch.equal(c.compute_amax(), quant_utils.reduce_amax(torch.max(x1, x2), axis=(1, 2, 3)))
+        c.reset()
+        assert c.compute_amax() is None
+
+    def test_track_amax(self, gpu):
+        import numpy as np
+
+        c = _calib(gpu).MaxCalibrator(8, None, False, track_amax=True)
+        x1, x2 = torch.rand(16).cuda(), torch.rand(16).cuda()
+        c.collect(x1)
+        c.collect(x2)
+        assert torch.equal(c.compute_amax(), torch.max(x1.max(), x2.max()))
+        np.testing.assert_array_equal(c.amaxs[0], x1.max().cpu().numpy())
+        np.testing.assert_array_equal(c.amaxs[1], x2.max().cpu().numpy())
+
+    def test_track_amax_raises(self, gpu):
+        c = _calib(gpu).MaxCalibrator(8, 0, False)
+        c.collect(torch.rand(3, 4, 2, 2).cuda())
+        with pytest.raises(RuntimeError, match="shape changed"):
+            c.collect(torch.rand(4, 4, 2, 2).cuda())
+
+
+def _hist_pair(gpu, *args, **kwargs):
+    """(device calibrator, oracle calibrator) with the same arguments."""
+    num_bits, _axis, unsigned = args
+    dev = _calib(gpu).HistogramCalibrator(num_bits, None, unsigned, **kwargs)
+    kw = {k: v for k, v in kwargs.items() if k in ("num_bins", "skip_zeros")}
+    ref = R.HistogramCalibratorRef(num_bits, unsigned, **kw)
+    return dev, ref
+
+
+class TestHistogramCalibrator:
+    def test_skip_zeros(self, gpu):
+        dev, ref = _hist_pair(gpu, 8, None, False, num_bins=2048, skip_zeros=True)
+        for x in (torch.tensor([0, 0, 0, 0, 0, 1, 2, 3, 4, 5]), torch.tensor([0, 0, 0, 0, 0, 6, 7, 8, 9, 10])):
+            dev.collect(x.cuda())
+            ref.collect(x)
+        amax = dev.compute_amax("percentile", percentile=50, start_bin=128)
+        assert (amax - 5.0).abs() < 10 / 2048
+        assert float(amax) == float(ref.compute_amax("percentile", percentile=50, start_bin=128))
+
+    def test_torch_hist_growth(self, gpu):
+        """test_torch_hist (test_calibrator.py:141-181): histogram / edges through range growth,
+        here against the oracle's torch-branch restatement (the numpy branch is not built)."""
+        torch.manual_seed(0)
+        x1 = torch.rand(15)
+        x1[0] = 0
+        x2 = torch.rand(15) + 1
+        x2[1] = 0
+        dev, ref = _hist_pair(gpu, 8, None, False, num_bins=19)
+        for x in [x1] + [x2, x1] * 3:
+            dev.collect(x.cuda())
+            ref.collect(x)
+            assert dev._calib_hist.numel() == dev._calib_bin_edges.numel() - 1
+            assert torch.equal(dev._calib_hist.cpu(), ref._calib_hist.cpu())
+            assert torch.allclose(dev._calib_bin_edges.cpu().double(), ref._calib_bin_edges.cpu().double())
+        dev.compute_amax("percentile", percentile=99.99)
+
+
+class TestEntropyCalibrator:
+    @pytest.mark.parametrize("unsigned", [False, True])
+    def test_one_tensor(self, gpu, unsigned):
+        dev, ref = _hist_pair(gpu, 8, None, unsigned, num_bins=512, grow_method="stretch")
+        x = torch.rand(11, 7, 3, 3)
+        x[1, 1, 1, 1] = 10.0
+        dev.collect(x.cuda())
+        ref.collect(x)
+        amax = dev.compute_amax("entropy", start_bin=32)
+        assert amax < 1.1
+        assert float(amax) == float(ref.compute_amax("entropy", start_bin=32))
+
+    def test_two_tensor(self, gpu):
+        dev = _calib(gpu).HistogramCalibrator(8, None, False, num_bins=512)
+        x2 = torch.rand(11, 7, 3, 3)
+        x2[1, 1, 1, 1] = 10.0
+        dev.collect(x2.cuda())
+        dev.collect(torch.rand(11, 7, 3, 3).cuda())
+        assert dev.compute_amax("entropy", start_bin=32) < 1.1
+
+    def test_repr(self, gpu):
+        repr(_calib(gpu).HistogramCalibrator(8, None, True, num_bins=2048))
+
+
+class TestMSECalibrator:
+    def test_one_tensor(self, gpu):
+        c = _calib(gpu).HistogramCalibrator(8, None, False, num_bins=32)
+        x = torch.ones(4, 4, 4) * 255.0
+        x[1, 1, 1] = 256.0
+        c.collect(x.cuda())
+        amax = c.compute_amax("mse", start_bin=16)
+        assert (amax - 255.0).abs() < (amax - 256.0).abs()
+
+    def test_unsigned_one_tensor(self, gpu):
+        c = _calib(gpu).HistogramCalibrator(8, None, True, num_bins=32)
+        x = torch.ones(11, 7, 3, 3) * 512.0
+        x[1, 1, 1, 1] = 513.0
+        c.collect(x.cuda())
+        amax = c.compute_amax("mse", start_bin=8)
+        assert (amax - 512.0).abs() < (amax - 513.0).abs()
+
+    def test_two_tensor(self, gpu):
+        c = _calib(gpu).HistogramCalibrator(8, None, False)
+        x1 = torch.ones(11, 7, 3, 3) * 255.0
+        x1[1, 1, 1, 1] = 256.0
+        c.collect(x1.cuda())
+        c.collect((torch.ones(11, 7, 3, 3) * 255.0).cuda())
+        amax = c.compute_amax("mse")
+        assert (amax - 255.0).abs() < (amax - 256.0).abs()
+
+
+class TestPercentileCalibrator:
+    @pytest.mark.parametrize(("unsigned", "pct", "want", "tol"), [(False, 90, 89.0, 100 / 1024), (True, 80, 79.0, 100 / 2048)])
+    def test_one_tensor(self, gpu, unsigned, pct, want, tol):
+        dev, ref = _hist_pair(gpu, 8, None, unsigned)
+        x = torch.arange(100)
+        dev.collect(x.cuda())
+        ref.collect(x.float())
+        amax = dev.compute_amax("percentile", percentile=pct)
+        assert (amax - want).abs() < tol
+        assert float(amax) == float(ref.compute_amax("percentile", percentile=pct))
+
+    def test_two_tensor(self, gpu):
+        c = _calib(gpu).HistogramCalibrator(8, None, False)
+        c.collect(torch.arange(100).cuda())
+        c.collect(torch.arange(0, 50, 0.5).cuda())
+        amax = c.compute_amax("percentile", percentile=99)
+        assert (amax - 97.0).abs() < 100 / 1024
+
+    def test_range(self, gpu):
+        c = _calib(gpu).HistogramCalibrator(8, None, False)
+        c.collect(torch.arange(100).cuda())
+        with pytest.raises(ValueError, match="range"):
+            c.compute_amax("percentile", percentile=-10)
+        with pytest.raises(ValueError, match="range"):
+            c.compute_amax("percentile", percentile=200)
