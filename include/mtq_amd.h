@@ -166,6 +166,21 @@ int mtq_nvfp4_fake_quant(const void *x, void *y, int64_t rows, int64_t cols, int
 int mtq_fp4_block_scale_quant(const void *x, void *y, int64_t nblocks, int block, int dtype,
                               const float *scales, hipStream_t stream);
 
+/* ---- QuantLinear simulated GEMM, short inputs (MFMA) ---------------------------------------
+ * Replaces, for M <= 16 input rows, the fake-quantised linear of the reference
+ * (nn/modules/quant_module.py:257-278 QuantLinearConvBase.forward + quant_linear.py:38-53:
+ * F.linear(x, weight_quantizer(W), b)) with one kernel that applies the weight fake quant to the
+ * MFMA operands in registers: y[M, N] = x[M, K] . qdq(W)[N, K]^T (+ bias[N]), dtype bf16 or f16
+ * (x, W, bias, y alike), fp32 accumulation (v_mfma_f32_16x16x32), one rounding of y.
+ * qdq(W): kind 0 = INT-n (num_bits, is_unsigned, narrow_range; as mtq_fake_tensor_quant_with_axis),
+ * kind 1 = FP8 e4m3 (as mtq_fake_e4m3fy_with_axis); amax_numel == 1 per tensor, else one amax per
+ * `block` consecutive elements of row-major W (block == K: per output channel; block % 32 == 0).
+ * Requires N % 16 == 0, K % 32 == 0, 16-byte aligned x and W; bias may be NULL. */
+int mtq_qlinear_small_m(const void *x, const void *w, const void *bias, void *y, int64_t M,
+                        int64_t N, int64_t K, int dtype, const void *amax, int amax_dtype,
+                        int64_t amax_numel, int64_t block, int kind, int num_bits,
+                        int is_unsigned, int narrow_range, hipStream_t stream);
+
 /* ---- checkpoint export (real-quant packing) ----------------------------------------------
  * export/quant_utils.py:836-938 to_quantized_weight and the qtensor quantize() routines; weights
  * [rows, cols] row-major of dtype, outputs raw bytes.

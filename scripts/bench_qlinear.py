@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Decode-shaped QuantLinear forward: fused MFMA kernel vs the reference's unfused path.
+
+One Llama-3-8B decoder layer's seven linears (q 4096x4096, k/v 1024x4096, o 4096x4096,
+gate/up 14336x4096, down 4096x14336: 218 M weights, 436 MB bf16 -- larger than the 256 MB
+Infinity Cache, so every pass streams W from HBM) at M = 1 / 4 / 16 input rows:
+
+  fused    ops.qlinear_small_m: weight fake quant applied to the MFMA operands (one pass over W)
+  unfused  the reference's QuantLinear forward: W_q = qdq(W) (read W, write W_q), then
+           F.linear(x, W_q) on hipBLASLt (read W_q)
+  bf16     F.linear(x, W) without quantization (hipBLASLt), the floor for any simulated GEMM
+
+Reported per config and M: ms per layer (7 linears), the weight bytes / time of the fused path
+as GB/s and fraction of the 8 TB/s HBM peak, and the speed-up over the unfused path.
+
+    python scripts/bench_qlinear.py [--iters 50]
+"""
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "tensorrt-model-optimizer_amd"))
+sys.path.insert(0, str(REPO))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+SHAPES = [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 14336)]
+
+
+def timed(fn, iters, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--per-linear-only", action="store_true")
+    a = ap.parse_args()
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    ws = [torch.randn(n, k, device="cuda", dtype=torch.bfloat16, generator=g) * 0.02 for n, k in SHAPES]
+    wbytes = sum(w.numel() * 2 for w in ws)
+    configs = {
+        # kind, num_bits, block, amax per weight
+        "int4_block128 (INT4_AWQ weights)": (0, 4, 128, [w.float().reshape(-1, 128).abs().amax(1, keepdim=True) for w in ws]),
+        "fp8_per_tensor (FP8_DEFAULT weights)": (1, 8, None, [w.float().abs().amax().reshape(()) for w in ws]),
+        "int8_per_channel (INT8_DEFAULT weights)": (0, 8, None, [w.float().abs().amax(1, keepdim=True) for w in ws]),
+    }
+    res = {"layer": "Llama-3-8B decoder layer, 7 linears, 218 M weights bf16", "weight_bytes": wbytes, "results": {}}
+    for m in (1, 4, 16):
+        xs = {k: torch.randn(m, k, device="cuda", dtype=torch.bfloat16, generator=g) for k in (4096, 14336)}
+
+        def bf16():
+            for w in ws:
+                F.linear(xs[w.shape[1]], w)
+
+        t_bf16 = timed(bf16, a.iters)
+        res["results"][f"M={m}"] = {"bf16_F.linear_ms": round(t_bf16, 4)}
+        for name, (kind, nb, block, amaxs) in ([] if a.per_linear_only else configs.items()):
+            blocks = [block or w.shape[1] for w in ws]
+
+            def fused():
+                for w, am, b in zip(ws, amaxs, blocks):
+                    ops.qlinear_small_m(xs[w.shape[1]], w, None, am, b, kind, nb, False, False)
+
+            def unfused():
+                for w, am, b in zip(ws, amaxs, blocks):
+                    if am.numel() == 1:
+                        wq = ops.quantize_op(w, am, nb, 4 if kind else 0, False, False)
+                    else:
+                        wq = ops.quantize_op(w.view(-1, b), am, nb, 4 if kind else 0, False, False).view_as(w)
+                    F.linear(xs[w.shape[1]], wq)
+
+            t_f, t_u = timed(fused, a.iters), timed(unfused, a.iters)
+            gbs = wbytes / (t_f * 1e-3) / 1e9
+            res["results"][f"M={m}"][name] = {
+                "fused_ms": round(t_f, 4), "unfused_ms": round(t_u, 4), "speedup": round(t_u / t_f, 2),
+                "fused_weight_GB_s": round(gbs, 1), "fused_frac_hbm": round(gbs / 8000.0, 4),
+            }
+        # per-linear split of the fused INT4 path (launch / latency-bound small matrices)
+        kind, nb, block, amaxs = configs["int4_block128 (INT4_AWQ weights)"]
+        per = {}
+        for i, (w, am) in enumerate(zip(ws, amaxs)):
+            t = timed(lambda: ops.qlinear_small_m(xs[w.shape[1]], w, None, am, 128, 0, 4, False, False), a.iters)
+            per[f"{i}:{w.shape[0]}x{w.shape[1]}"] = [round(t * 1e3, 1), round(w.numel() * 2 / (t * 1e-3) / 1e9, 1)]
+        res["results"][f"M={m}"]["int4_fused_per_linear_us_GBs"] = per
+        print(json.dumps({f"M={m}": res["results"][f"M={m}"]}), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

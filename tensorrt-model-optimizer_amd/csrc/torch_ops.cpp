@@ -562,6 +562,41 @@ at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at:
   return y;
 }
 
+// QuantLinear simulated GEMM for short inputs: y = x . qdq(W)^T (+ bias), weight fake quant fused
+// into the MFMA operand loads (mtq_qlinear_small_m).  kind 0 = INT-n, 1 = FP8 e4m3.
+at::Tensor qlinear_small_m(const at::Tensor &input, const at::Tensor &weight,
+                           const c10::optional<at::Tensor> &bias, const at::Tensor &amax,
+                           int64_t block, int64_t kind, int64_t num_bits, bool is_unsigned,
+                           bool narrow_range) {
+  check_device(input, "input");
+  check_device(weight, "weight");
+  TORCH_CHECK(weight.dim() == 2, "qlinear_small_m: 2-D weight expected");
+  TORCH_CHECK(input.scalar_type() == weight.scalar_type(), "qlinear_small_m: input/weight dtype mismatch");
+  const int dt = checked_dtype(input, "input");
+  const int64_t N = weight.size(0), K = weight.size(1);
+  TORCH_CHECK(input.size(-1) == K, "qlinear_small_m: input last dim must equal weight.size(1)");
+  at::Tensor x = input.contiguous();
+  at::Tensor w = weight.contiguous();
+  const int64_t M = K ? x.numel() / K : 0;
+  at::Tensor a = amax.contiguous();
+  TORCH_CHECK(a.device() == x.device(), "qlinear_small_m: amax must be on the input device");
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->contiguous();
+    TORCH_CHECK(b.scalar_type() == x.scalar_type() && b.numel() == N, "qlinear_small_m: bias");
+  }
+  std::vector<int64_t> shape(input.sizes().begin(), input.sizes().end());
+  shape.back() = N;
+  at::Tensor y = at::empty(shape, x.options());
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  int st = mtq_qlinear_small_m(x.data_ptr(), w.data_ptr(), b.defined() ? b.data_ptr() : nullptr,
+                               y.data_ptr(), M, N, K, dt, a.data_ptr(), checked_dtype(a, "amax"),
+                               a.numel(), block, (int)kind, (int)num_bits, is_unsigned, narrow_range,
+                               cur_stream(x));
+  check_status(st, "qlinear_small_m");
+  return y;
+}
+
 void histogram_abs_accumulate(const at::Tensor &inputs, const at::Tensor &hmax, at::Tensor counts,
                               int64_t bins, bool skip_zeros) {
   at::Tensor x = inputs.contiguous();
@@ -661,6 +696,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "bool unsigned, bool narrow_range) -> Tensor");
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
         "bool skip_zeros) -> ()");
+  m.def("qlinear_small_m(Tensor input, Tensor weight, Tensor? bias, Tensor amax, int block, int kind, "
+        "int num_bits, bool unsigned, bool narrow_range) -> Tensor");
   m.def("mse_accumulate(Tensor a, Tensor b, Tensor(a!) loss, int index) -> ()");
   m.def("mul_cols(Tensor inputs, Tensor scale) -> Tensor");
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
@@ -679,6 +716,7 @@ TORCH_LIBRARY(modelopt_amd, m) {
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("quantize_op", &quantize_op);
+  m.impl("qlinear_small_m", &qlinear_small_m);
   m.impl("dynamic_block_quantize_op", &dynamic_block_quantize_op);
   m.impl("fake_tensor_quant", &fake_tensor_quant);
   m.impl("fake_tensor_quant_", &fake_tensor_quant_);
@@ -704,6 +742,12 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {
+  m.impl("qlinear_small_m", [](const at::Tensor &x, const at::Tensor &w, const c10::optional<at::Tensor> &,
+                               const at::Tensor &, int64_t, int64_t, int64_t, bool, bool) {
+    std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+    shape.back() = w.size(0);
+    return at::empty(shape, x.options().device(at::kMeta));
+  });
   m.impl("quantize_op", [](const at::Tensor &x, const at::Tensor &, int64_t, int64_t, bool, bool) {
     return meta_like(x);
   });

@@ -1,11 +1,97 @@
-"""Quantized Linear (reference: nn/modules/quant_linear.py:38-53)."""
+"""Quantized Linear (reference: nn/modules/quant_linear.py:38-53).
 
+MI355X addition: for short inputs (<= 16 rows after flattening, decode / small-batch evaluation
+of a quantized model) the forward runs the fused MFMA kernel ``qlinear_small_m``, which applies
+the weight fake quant to the GEMM operands in registers instead of writing a dequantised copy of
+the weight to HBM and reading it back (one pass over W instead of three).  The dequantised weight
+values are bit-identical to the unfused path (same qdq helpers); only the GEMM summation order
+differs.  Gradients, calibration, dynamic / MX / NVFP4 / custom-backend weight quantizers and
+long inputs take the reference's path.  ``MTQ_AMD_FUSED_QLINEAR=0`` disables the fusion.
+"""
+
+import os
+
+import torch
 import torch.nn as nn
+
+from modelopt_amd._ext import ops as _ops
 
 from ... import tensor_quant
 from .quant_module import QuantLinearConvBase, QuantModuleRegistry
+from .tensor_quantizer import StaticBlockScaleQuantizer, TensorQuantizer
 
 __all__ = ["Linear", "QuantLinear"]
+
+_FUSED_MAX_ROWS = 16
+_FUSED = [os.environ.get("MTQ_AMD_FUSED_QLINEAR", "1") != "0"]
+
+
+def _fused_weight_params(wq, weight):
+    """(amax, block, kind) when ``wq``'s fake quant of ``weight`` is an element-wise INT-n / FP8
+    qdq with a per-tensor, per-output-channel or 1-D static-block (along K) amax; else None."""
+    if type(wq) not in (TensorQuantizer, StaticBlockScaleQuantizer):
+        return None
+    if wq._disabled or not wq._if_quant or wq._if_calib or not wq._fake_quant or wq._dynamic:
+        return None
+    if wq.backend is not None or wq.pre_quant_scale is not None or wq.is_mx_format:
+        return None
+    if isinstance(wq, StaticBlockScaleQuantizer) and wq.is_nvfp4_static:
+        return None
+    amax = getattr(wq, "_amax", None)
+    if amax is None or amax.device != weight.device or amax.numel() < 1:
+        return None
+    nb = wq._num_bits
+    if nb == (4, 3):
+        kind = 1
+    elif isinstance(nb, int) and not isinstance(nb, bool):
+        kind = 0
+    else:
+        return None
+    n, k = weight.shape
+    bs = wq._block_sizes
+    if amax.numel() == 1:
+        return amax, k, kind
+    if not bs and amax.numel() == n and tuple(amax.shape) in ((n, 1), (n,)):
+        return amax, k, kind  # per output channel (axis 0)
+    if bs and set(bs) <= {-1, 1, "type"} and bs.get("type", "static") == "static":
+        b = bs.get(-1) or bs.get(1)
+        if b and k % b == 0 and b % 32 == 0 and amax.numel() * b == n * k:
+            return amax, b, kind
+    return None
+
+
+def _fused_forward(mod, input):
+    """The fused short-input forward, or None when the module/input does not qualify."""
+    if not _FUSED[0] or input.device.type != "cuda" or input.dtype not in (torch.bfloat16, torch.float16):
+        return None
+    weight = mod._parameters.get("weight")
+    if weight is None or weight.dtype != input.dtype or weight.dim() != 2:
+        return None
+    n, k = weight.shape
+    if input.shape[-1] != k or k % 32 or n % 16 or input.numel() // max(k, 1) > _FUSED_MAX_ROWS:
+        return None
+    if torch.is_grad_enabled() and (input.requires_grad or weight.requires_grad):
+        return None
+    wq, oq = mod._modules.get("weight_quantizer"), mod._modules.get("output_quantizer")
+    if oq is not None and oq.is_enabled:
+        return None
+    p = _fused_weight_params(wq, weight)
+    if p is None:
+        return None
+    amax, block, kind = p
+    bias = mod._parameters.get("bias")
+    if bias is not None and bias.dtype != input.dtype:
+        return None
+    x = mod.input_quantizer(input)
+    if x.dtype != input.dtype:
+        return None
+    x = x.contiguous()
+    if x.data_ptr() % 16:
+        x = x.clone()  # the MFMA operand loads are 16-byte vectors
+    return _ops().qlinear_small_m(
+        x, weight, bias, amax, block, kind, wq._num_bits if kind == 0 else 8, bool(wq._unsigned),
+        bool(wq._narrow_range),
+    )
 
 
 @QuantModuleRegistry.register({nn.Linear: "nn.Linear"})
@@ -13,6 +99,13 @@ class _QuantLinear(QuantLinearConvBase):
     """Quantized base class for nn.Linear type classes: weight per-row INT8 by default."""
 
     default_quant_desc_weight = tensor_quant.QUANT_DESC_8BIT_LINEAR_WEIGHT_PER_ROW
+
+    def forward(self, input, *args, **kwargs):
+        if not args and not kwargs:
+            y = _fused_forward(self, input)
+            if y is not None:
+                return y
+        return super().forward(input, *args, **kwargs)
 
     @staticmethod
     def quantized_linear_fn(package, func_name, self, input, weight, *args, **kwargs):
