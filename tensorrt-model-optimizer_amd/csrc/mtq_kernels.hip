@@ -1713,23 +1713,42 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_kernel(const T *__restr
 
 
 // ---- vectorised export packing (one 16 B input vector per lane, chunked non-temporal) --------
-template <int NB> struct ByteVec;
-template <> struct ByteVec<2> { using type = uint16_t; };
-template <> struct ByteVec<4> { using type = uint32_t; };
-template <> struct ByteVec<8> { using type = uint2; };
+// Index math: with IDX32 (every vector index < 2^31, true for any single weight up to 16 G
+// elements of bf16) the row / block of a vector comes from a 32-bit multiply-high divider
+// (make_fastdiv) instead of a 64-bit division (~40 VALU ops per lane); packed bytes go out with
+// non-temporal stores like the fake-quant kernels' outputs.
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_packed_nt(uint8_t *p, uint32_t o) {
+  __builtin_nontemporal_store(o, reinterpret_cast<uint32_t *>(p));
+}
+__device__ __forceinline__ void st_packed_nt(uint8_t *p, uint16_t o) {
+  __builtin_nontemporal_store(o, reinterpret_cast<uint16_t *>(p));
+}
+__device__ __forceinline__ void st_packed_nt(uint8_t *p, uint32_t lo, uint32_t hi) {
+  u32x2_t o = {lo, hi};
+  __builtin_nontemporal_store(o, reinterpret_cast<u32x2_t *>(p));
+}
 
-template <typename T>
-__global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__restrict__ x,
+template <bool IDX32>
+__device__ __forceinline__ int64_t idx_div(int64_t n, int64_t d, const FastDiv &f) {
+  if constexpr (IDX32)
+    return (int64_t)fdiv((uint32_t)n, f);
+  else
+    return n / d;
+}
+
+template <typename T, bool IDX32>
+__device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restrict__ x,
                                                                    uint8_t *__restrict__ y,
-                                                                   int64_t nvec, int64_t cols,
+                                                                   int64_t nvec, int64_t cv,
+                                                                   FastDiv fcv,
                                                                    const float *__restrict__ scale,
                                                                    int per_row, int round_dtype) {
   using V = Vec<T>;
   constexpr int N = V::N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= nvec) return;
   V v = ldg_vec_nt(x + i * N);
-  const float s = scale[per_row ? (i * N) / cols : 0];
+  const float s = scale[per_row ? idx_div<IDX32>(i, cv, fcv) : 0];
   const float r = 1.0f / s;
   uint32_t b[N];
 #pragma unroll
@@ -1738,32 +1757,30 @@ __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__res
     if (round_dtype) q = Elem<T>::ld(Elem<T>::st(q));
     b[j] = e4m3_byte(q);
   }
-  if constexpr (N == 8) {
-    uint2 o;
-    o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-    o.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
-    *reinterpret_cast<uint2 *>(y + i * N) = o;
-  } else {
-    *reinterpret_cast<uint32_t *>(y + i * N) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-  }
+  if constexpr (N == 8)
+    st_packed_nt(y + i * N, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
+                 b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
+  else
+    st_packed_nt(y + i * N, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
 }
 
 // rows (2p, 2p+1) x N columns -> N bytes
-template <typename T>
-__global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__restrict__ x,
+template <typename T, bool IDX32>
+__device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restrict__ x,
                                                                     uint8_t *__restrict__ y,
                                                                     int64_t nvec, int64_t cols,
+                                                                    FastDiv fcv, FastDiv fblk,
                                                                     const float *__restrict__ scale,
                                                                     int64_t nblk, int block) {
   using V = Vec<T>;
   constexpr int N = V::N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;  // over (rows/2) * cols / N
   if (i >= nvec) return;
   const int64_t cv = cols / N;
-  const int64_t pr = i / cv, c0 = (i - pr * cv) * N;
+  const int64_t pr = idx_div<IDX32>(i, cv, fcv), c0 = (i - pr * cv) * N;
   V lo = ldg_vec_nt(x + (2 * pr) * cols + c0);
   V hi = ldg_vec_nt(x + (2 * pr + 1) * cols + c0);
-  const float s0 = scale[(2 * pr) * nblk + c0 / block], s1 = scale[(2 * pr + 1) * nblk + c0 / block];
+  const int64_t cb = idx_div<IDX32>(c0, block, fblk);
+  const float s0 = scale[(2 * pr) * nblk + cb], s1 = scale[(2 * pr + 1) * nblk + cb];
   const float r0 = 1.0f / s0, r1 = 1.0f / s1;
   uint32_t b[N];
 #pragma unroll
@@ -1775,29 +1792,26 @@ __global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__re
     const int v0 = q0 != q0 ? 0 : (int)q0, v1 = q1 != q1 ? 0 : (int)q1;
     b[j] = ((uint32_t)v0 & 0xFu) | (((uint32_t)v1 & 0xFu) << 4);
   }
-  if constexpr (N == 8) {
-    uint2 o;
-    o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-    o.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
-    *reinterpret_cast<uint2 *>(y + pr * cols + c0) = o;
-  } else {
-    *reinterpret_cast<uint32_t *>(y + pr * cols + c0) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-  }
+  if constexpr (N == 8)
+    st_packed_nt(y + pr * cols + c0, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
+                 b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
+  else
+    st_packed_nt(y + pr * cols + c0, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
 }
 
 // one 16 B vector (N elements of one block) -> N/2 bytes
-template <typename T>
-__global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__restrict__ x,
+template <typename T, bool IDX32>
+__device__ __forceinline__ void export_nvfp4_vec_one(int64_t i, const T *__restrict__ x,
                                                                      uint8_t *__restrict__ y,
-                                                                     int64_t nvec, int block,
+                                                                     int64_t nvec, int64_t vpb,
+                                                                     FastDiv fvpb,
                                                                      const float *__restrict__ sblk,
                                                                      const float *__restrict__ s2) {
   using V = Vec<T>;
   constexpr int N = V::N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= nvec) return;
   V v = ldg_vec_nt(x + i * N);
-  const float d = sblk[(i * N) / block] * (*s2);
+  const float d = sblk[idx_div<IDX32>(i, vpb, fvpb)] * (*s2);
   const float r = 1.0f / d;
   uint32_t o = 0;
 #pragma unroll
@@ -1807,22 +1821,21 @@ __global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__r
     o |= (lo | (hi << 4)) << (4 * j);
   }
   if constexpr (N == 8)
-    *reinterpret_cast<uint32_t *>(y + i * (N / 2)) = o;
+    st_packed_nt(y + i * (N / 2), o);
   else
-    *reinterpret_cast<uint16_t *>(y + i * (N / 2)) = (uint16_t)o;
+    st_packed_nt(y + i * (N / 2), (uint16_t)o);
 }
 
 // MXFP4: LPB = block / N lanes per block, shuffle-max, every lane writes N/2 code bytes, the
 // block's first lane its E8M0 byte.
 template <typename T, int BLOCK>
-__global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__restrict__ x,
+__device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const T *__restrict__ x,
                                                                      uint8_t *__restrict__ y,
                                                                      uint8_t *__restrict__ sc,
                                                                      int64_t nvec) {
   using V = Vec<T>;
   constexpr int N = V::N;
   constexpr int LPB = BLOCK / N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i - (threadIdx.x % LPB) >= nvec) return;
   V v = ldg_vec_nt(x + i * N);
   float amax = 0.f;
@@ -1849,10 +1862,78 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
     o |= (((q > 0.f) ? 0u : 8u) + ord) << (4 * j);
   }
   if constexpr (N == 8)
-    *reinterpret_cast<uint32_t *>(y + i * (N / 2)) = o;
+    st_packed_nt(y + i * (N / 2), o);
   else
-    *reinterpret_cast<uint16_t *>(y + i * (N / 2)) = (uint16_t)o;
+    st_packed_nt(y + i * (N / 2), (uint16_t)o);
 }
+
+// U consecutive 256-vector chunks per block (MTQ_AMD_EXPORT_U = 1, 2 or 4; default 2).
+template <int U, typename T, bool IDX32>
+__global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__restrict__ x,
+                                                                   uint8_t *__restrict__ y,
+                                                                   int64_t nvec, int64_t cv,
+                                                                   FastDiv fcv,
+                                                                   const float *__restrict__ scale,
+                                                                   int per_row, int round_dtype) {
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    export_fp8_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cv, fcv, scale, per_row, round_dtype);
+}
+template <int U, typename T, bool IDX32>
+__global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__restrict__ x,
+                                                                    uint8_t *__restrict__ y,
+                                                                    int64_t nvec, int64_t cols,
+                                                                    FastDiv fcv, FastDiv fblk,
+                                                                    const float *__restrict__ scale,
+                                                                    int64_t nblk, int block) {
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    export_int4_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cols, fcv, fblk, scale, nblk, block);
+}
+template <int U, typename T, bool IDX32>
+__global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__restrict__ x,
+                                                                     uint8_t *__restrict__ y,
+                                                                     int64_t nvec, int64_t vpb,
+                                                                     FastDiv fvpb,
+                                                                     const float *__restrict__ sblk,
+                                                                     const float *__restrict__ s2) {
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    export_nvfp4_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, vpb, fvpb, sblk, s2);
+}
+template <int U, typename T, int BLOCK>
+__global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__restrict__ x,
+                                                                     uint8_t *__restrict__ y,
+                                                                     uint8_t *__restrict__ sc,
+                                                                     int64_t nvec) {
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK>(base + u * kThreads, x, y, sc, nvec);
+}
+
+int export_u() {
+  static int u = -1;
+  if (u < 0) {
+    const char *e = getenv("MTQ_AMD_EXPORT_U");
+    u = e ? atoi(e) : 2;
+    if (u != 1 && u != 2 && u != 4) u = 2;
+  }
+  return u;
+}
+// calls f(std::integral_constant<int, U>) with the configured U
+template <class F> void with_export_u(F &&f) {
+  const int u = export_u();
+  if (u == 4)
+    f(std::integral_constant<int, 4>{});
+  else if (u == 1)
+    f(std::integral_constant<int, 1>{});
+  else
+    f(std::integral_constant<int, 2>{});
+}
+unsigned export_grid(int64_t nvec, int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); }
 
 }  // namespace
 
@@ -2169,9 +2250,20 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
     const int64_t n = rows * cols;
     constexpr int N = Vec<T>::N;
     if (cols % N == 0 && aligned16(x) && ((uintptr_t)y % N) == 0) {
-      const int64_t nvec = n / N;
-      export_fp8_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-          reinterpret_cast<const T *>(x), y, nvec, cols, scale, per_row, round_to_dtype);
+      const int64_t nvec = n / N, cv = cols / N;
+      const FastDiv fcv = make_fastdiv(cv < (1ll << 31) ? (uint32_t)cv : 1u);
+      if (nvec < (1ll << 31))
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_fp8_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype);
+        });
+      else
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_fp8_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype);
+        });
     } else {
       export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
           reinterpret_cast<const T *>(x), y, n, cols, scale, per_row, round_to_dtype);
@@ -2191,8 +2283,21 @@ int mtq_export_int4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int d
     constexpr int N = Vec<T>::N;
     if (cols % N == 0 && block % N == 0 && aligned16(x) && ((uintptr_t)y % N) == 0) {
       const int64_t nvec = n / N;
-      export_int4_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-          reinterpret_cast<const T *>(x), y, nvec, cols, scale, cols / block, block);
+      const bool i32 = nvec < (1ll << 31) && cols < (1ll << 31);
+      const FastDiv fcv = make_fastdiv(i32 ? (uint32_t)(cols / N) : 1u);
+      const FastDiv fblk = make_fastdiv((uint32_t)block);
+      if (i32)
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_int4_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), y, nvec, cols, fcv, fblk, scale, cols / block, block);
+        });
+      else
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_int4_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), y, nvec, cols, fcv, fblk, scale, cols / block, block);
+        });
     } else {
       export_int4_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
           reinterpret_cast<const T *>(x), y, rows / 2, cols, scale, cols / block, block);
@@ -2212,9 +2317,20 @@ int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int 
     const int64_t npairs = rows * cols / 2;
     constexpr int N = Vec<T>::N;
     if (block % N == 0 && aligned16(x) && ((uintptr_t)y % (N / 2)) == 0) {
-      const int64_t nvec = rows * cols / N;
-      export_nvfp4_vec_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-          reinterpret_cast<const T *>(x), y, nvec, block, block_scale, scale_2);
+      const int64_t nvec = rows * cols / N, vpb = block / N;
+      const FastDiv fvpb = make_fastdiv((uint32_t)vpb);
+      if (nvec < (1ll << 31))
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_nvfp4_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2);
+        });
+      else
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_nvfp4_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2);
+        });
     } else {
       export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
           reinterpret_cast<const T *>(x), y, npairs, cols, block_scale, scale_2, block);
@@ -2234,11 +2350,16 @@ int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int 
     constexpr int N = Vec<T>::N;
     if (aligned16(x) && ((uintptr_t)y % (N / 2)) == 0 && (block == 32 || block == 16) && block % N == 0) {
       const int64_t nvec = n / N;
-      const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
       if (block == 32)
-        export_mxfp4_vec_kernel<T, 32><<<g, kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_mxfp4_vec_kernel<U, T, 32><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+        });
       else
-        export_mxfp4_vec_kernel<T, 16><<<g, kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_mxfp4_vec_kernel<U, T, 16><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+        });
     } else {
       export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(
           reinterpret_cast<const T *>(x), y, scales, nb, block);
