@@ -25,6 +25,7 @@ Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.dis
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -335,7 +336,10 @@ def main():
         del xs, blk
         torch.cuda.empty_cache()
         _barrier(dist)
-        res = ptq_llama.run(samples=512, seq=512, rank=rank, world=world, baseline=(world == 1))
+        # the library's conversion messages (reference prints) go to stderr: stdout carries
+        # exactly one JSON line
+        with contextlib.redirect_stdout(sys.stderr):
+            res = ptq_llama.run(samples=512, seq=512, rank=rank, world=world, baseline=(world == 1))
         res["ptq_wall_clock_s"] = round(_max_over_ranks(dist, res["ptq_wall_clock_s"]), 3)
         res["calib_tokens_per_s"] = round(512 * 512 / res["ptq_wall_clock_s"], 1)
         out["ptq"] = res
