@@ -29,6 +29,8 @@ xs = [torch.randn(T, H, device="cuda", dtype=torch.bfloat16, generator=g) for _ 
 blk = [x.view(-1, B).abs().amax(dim=1, keepdim=True).float() for x in xs]
 amax = torch.tensor(8.0, device="cuda")
 acc = torch.zeros(1, device="cuda")
+hmax = torch.tensor([16.0 * 6], device="cuda")  # bench.py's histogram range
+counts = torch.zeros(2048, dtype=torch.int32, device="cuda")
 torch.cuda.synchronize()
 for i in range(args.iters):
     x = xs[i % 4]
@@ -40,6 +42,10 @@ for i in range(args.iters):
         ops.fake_tensor_quant(x, amax, 8, False, False)
     elif args.kernel == "mxfp4":
         ops.fused_amax_convert(x, 32, 6, 9, None)
+    elif args.kernel == "hist":
+        ops.histogram_abs_accumulate(x, hmax, counts, 2048, False)
+    elif args.kernel == "nvfp4":
+        ops.nvfp4_fake_quant_block(x, amax, 16)
     elif args.kernel == "amax":
         ops.amax_accumulate(x, acc, 1, 1, x.numel())
     else:

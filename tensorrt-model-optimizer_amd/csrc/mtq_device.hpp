@@ -6,7 +6,7 @@
 //  * `div_rn` is the correctly rounded fp32 quotient q/s computed from a correctly rounded
 //    reciprocal r = RN(1/s) with one FMA correction (Markstein).  Exhaustively checked on
 //    the host for every fp32 significand of s at 7 exponents x every q in [-128, 127] and
-//    for sampled 16-bit q (oracle/check_div_rn.c): bit-identical to q / s.  It replaces two
+//    for 16-bit q on every 64th significand (scripts/check_div_rn.c, run sliced by tests/test_div_rn_check.py): bit-identical to q / s.  It replaces two
 //    ~12-instruction IEEE divisions per element by 3 instructions, which keeps the INT-n
 //    qdq kernels HBM-bound (SURVEY.md §8a a9 requires `/scale`, not `*inv_scale`).
 //  * Clamps are written as compare-selects so NaN propagates like torch.clamp / the

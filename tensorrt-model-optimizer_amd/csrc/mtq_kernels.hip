@@ -1320,6 +1320,109 @@ __global__ __launch_bounds__(kHistDivThreads) void hist_div_kernel(
   }
 }
 
+// Value-histogram form (bf16 / f16, bins <= 8192; default for them).  |x| of a 16-bit float is
+// one of 32768 bit patterns, so a block first counts the patterns themselves in LDS (one
+// `and` + one `ds_add_u32` per element, no arithmetic), then folds the <= 32768 pattern counts
+// into its bins with the same exact bin formula as hist_div_kernel, evaluated once per distinct
+// pattern instead of once per element.  The bin of an element is a function of its pattern
+// only, so the counts equal the per-element kernel's exactly.  Measured on hist_div_kernel
+// (profiles/r02/histogram/): ~14 VALU instructions per element, LDS 46 % busy -- the per-element
+// bin arithmetic, not the LDS, was what this form removes.  LDS: 128 KiB pattern counts + the
+// bins, so one 1024-thread block per CU over one contiguous chunk.
+constexpr int kHistValThreads = 1024;
+constexpr int kHistPatterns = 32768;
+template <typename T, int U, bool PF>
+__global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
+    const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
+    int skip_zeros, uint32_t *counts) {
+  static_assert(sizeof(T) == 2, "pattern histogram is for 16-bit floats");
+  extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+  uint32_t *vh = sh;                  // [32768] counts per |x| bit pattern
+  uint32_t *bh = sh + kHistPatterns;  // [bins]
+  for (int i = threadIdx.x; i < kHistPatterns / 4; i += kHistValThreads)
+    reinterpret_cast<uint4 *>(vh)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int b = threadIdx.x; b < bins; b += kHistValThreads) bh[b] = 0;
+  const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
+  int64_t v1 = v0 + vec_per_block;
+  v1 = v1 < nvec ? v1 : nvec;
+  constexpr int64_t kStep = (int64_t)kHistValThreads * U;
+  // one U-vector batch per lane; past-the-end slots read as a NaN pattern (dropped by the fold)
+  auto load = [&](int64_t i, uint4 (&v)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + (int64_t)u * kHistValThreads;
+      if (k < v1) {
+        const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + k * 8));
+        v[u] = make_uint4(r.x, r.y, r.z, r.w);
+      } else {
+        v[u] = make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
+      }
+    }
+  };
+  auto count = [&](const uint4 (&v)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        atomicAdd(vh + (w[j] & 0x7FFFu), 1u);
+        atomicAdd(vh + ((w[j] >> 16) & 0x7FFFu), 1u);
+      }
+    }
+  };
+  int64_t i = v0 + threadIdx.x;
+  if constexpr (PF) {
+    // register double buffer: the next batch's loads are in flight while this one is counted
+    uint4 cur[U];
+    load(i, cur);
+    __syncthreads();  // LDS zeroed (after the first loads were issued)
+    for (; i < v1; i += kStep) {
+      uint4 nxt[U];
+      if (i + kStep < v1) load(i + kStep, nxt);
+      count(cur);
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+  } else {
+    __syncthreads();
+    for (; i < v1; i += kStep) {
+      uint4 v[U];
+      load(i, v);
+      count(v);
+    }
+  }
+  __syncthreads();
+  // fold: pattern -> bin (torch.histc formula, hist_div_kernel's exact division)
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  const float fb = (float)bins;
+  const float span = hi - lo;
+  const float y = 1.f / span;
+  const uint32_t last = (uint32_t)bins - 1u;
+  for (int p = threadIdx.x; p < kHistPatterns; p += kHistValThreads) {
+    const uint32_t c = vh[p];
+    if (c == 0u) continue;
+    const uint16_t bits = (uint16_t)p;
+    T tv;
+    __builtin_memcpy(&tv, &bits, 2);
+    const float a = Elem<T>::ld(tv);
+    if (a <= hi && !(skip_zeros && a == 0.f)) {  // NaN patterns fail the compare
+      const float t = (a - lo) * fb;
+      const float q0 = t * y;
+      const float q = __builtin_fmaf(__builtin_fmaf(-q0, span, t), y, q0);
+      uint32_t b = (uint32_t)(int)q;
+      b = b < last ? b : last;
+      atomicAdd(bh + b, c);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < bins; b += kHistValThreads)
+    if (bh[b]) atomicAdd(counts + b, bh[b]);
+}
+
 // ============================================================================================
 // AWQ-lite search helpers: column scale (x * s[col]) and the per-alpha MSE loss
 // ============================================================================================
@@ -2114,11 +2217,45 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
     const size_t shm = lds ? (size_t)bins * 4 : 0;
     static int hv = -1;
     const int var = env_variant("MTQ_AMD_HIST_VARIANT", &hv);
+    // 16-bit dtypes: pattern histogram + per-block fold.  Variants measured on bf16
+    // [32768, 4096], 2048 bins (profiles/r02/histogram/): 0 = U 2 with register prefetch
+    // 46.9 us (71.6 %); 20 = U 4 no prefetch 48.4; 21 = U 4 prefetch 49.6; 22 = U 8 prefetch
+    // 54.1; 23 = U 1 prefetch 56.5; 24 = U 2 no prefetch 46.8-47.3.
+    if constexpr (sizeof(T) == 2) {
+      if ((var == 0 || (var >= 20 && var <= 24)) && aligned16(x) && n % N == 0 && bins <= 8192) {
+        const int64_t nvec = n / N;
+        int64_t blocks = num_cus();
+        const int64_t min_per_block = (int64_t)kHistValThreads * 8;
+        int64_t vpb = (nvec + blocks - 1) / blocks;
+        vpb = vpb < min_per_block ? min_per_block : vpb;
+        blocks = (nvec + vpb - 1) / vpb;
+        const size_t shr = ((size_t)kHistPatterns + (size_t)bins) * 4;
+        auto go = [&](auto kern, int slot) {
+          static bool attr[6] = {false, false, false, false, false, false};  // per kernel
+          if (!attr[slot]) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr[slot] = true;
+          }
+          kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins,
+                                                                   skip_zeros, counts);
+          return check_launch();
+        };
+        if (var == 20) return go(hist_value_kernel<T, 4, false>, 1);
+        if (var == 21) return go(hist_value_kernel<T, 4, true>, 2);
+        if (var == 22) return go(hist_value_kernel<T, 8, true>, 3);
+        if (var == 23) return go(hist_value_kernel<T, 1, true>, 4);
+        if (var == 24) return go(hist_value_kernel<T, 2, false>, 5);
+        return go(hist_value_kernel<T, 2, true>, 0);
+      }
+    }
     // variants (MTQ_AMD_HIST_VARIANT, scripts/sweep_reduce.py): 0 = REP 4, 2 blocks per CU
     // (4.3 TB/s on bf16 [32768, 4096]); 8 = REP 8, 1 block per CU; 9 = REP 8, 2 per CU;
     // 1 = the plain LDS-privatised kernels below (2.4 TB/s, VALU-bound on the division)
-    if ((var == 0 || var == 8 || var == 9) && aligned16(x) && n % N == 0 && bins <= 16384) {
-      int rep = var == 0 ? 4 : 8;
+    // (10 = the REP-4 division kernel for 16-bit dtypes too; fp32 and > 8192 bins land here)
+    if ((var == 0 || var == 8 || var == 9 || var == 10 || var == 20) && aligned16(x) &&
+        n % N == 0 && bins <= 16384) {
+      int rep = (var == 8 || var == 9) ? 8 : 4;
       while (rep > 1 && (int64_t)bins * rep > 16384) rep >>= 1;
       const int per_cu = var == 8 ? 1 : 2;
       const int64_t nvec = n / N;

@@ -586,70 +586,62 @@ class TensorQuantizer(nn.Module):
         )
 
     # ---- static block quant reshapes (reference :975-1085) ------------------------------------
+    # Semantics (pinned by the padding goldens, tests/test_gpu_golden.py): every blocked axis is
+    # right-padded with zeros to a multiple of its block and split into (n_blocks, block); the
+    # block dims are reduced, every other dim is kept.  A single block on the last dim is the
+    # common case and becomes the flat (-1, block) view with axis (0,) -- the layout the HIP
+    # kernels and the reference's export amax reshape expect.
+    def _block_plan(self, shape: torch.Size) -> list[tuple[int, int | None, int]]:
+        """Per input dim: (extent, block size or None, right padding)."""
+        nd = len(shape)
+        plan = []
+        for d, n in enumerate(shape):
+            b = self.block_sizes.get(d, self.block_sizes.get(d - nd, None))
+            plan.append((n, b, (-n) % b if b else 0))
+        return plan
+
     def _setup_for_blockquant(self, inputs: torch.Tensor):
-        def get_axis_quant_params(ax):
-            ax = ax if ax in self.block_sizes else ax - inputs.dim()
-            bsize = self.block_sizes.get(ax, None)
-            padding, ax_slice = None, None
-            if bsize is not None and inputs.shape[ax] % bsize != 0:
-                padding = (bsize - (inputs.shape[ax] % bsize), 0)
-                ax_slice = slice(inputs.shape[ax])
-            return bsize, padding, ax_slice
-
-        def set_quant_params(axis, block_reshape_size, padding, slices, amax_shape=None):
-            self._axis = tuple(axis)
-            if hasattr(self, "_calibrator"):
-                self._calibrator._axis = self._axis
-            self._original_shape = inputs.shape
-            self._block_reshape_size = torch.Size(block_reshape_size)
-            if padding is not None:
-                self._padding = tuple(padding)
-                self._original_shape = F.pad(inputs, self._padding, "constant", 0).shape
-            if slices is not None:
-                self._slices = slices
-            if amax_shape:
-                self._amax_shape_for_export = amax_shape
-
         if hasattr(self, "_block_reshape_size"):
-            return
+            return  # the layout is fixed by the first call (reference behaviour)
+        shape = inputs.shape
+        plan = self._block_plan(shape)
+        blocked = [d for d, (_, b, _) in enumerate(plan) if b]
+        n_block_axes = len(QuantizerAttributeConfig._get_block_quant_axes_and_sizes(self.block_sizes))
+        last_only = n_block_axes == 1 and blocked == [len(shape) - 1]
 
-        reshape_size, quantize_axis, paddings, slices = [], [], [], []
-        if (self.block_sizes.get(inputs.dim() - 1, None) or self.block_sizes.get(-1, None)) and len(
-            QuantizerAttributeConfig._get_block_quant_axes_and_sizes(self.block_sizes)
-        ) == 1:
-            bsize, padding, ax_slice = get_axis_quant_params(inputs.dim() - 1)
-            slices = None if ax_slice is None else (*(slice(None),) * (inputs.dim() - 1), ax_slice)
-            padding = padding if not padding else tuple(reversed(padding))
-            amax_shape_for_export = (*(inputs.shape[:-1]), -1)
-            set_quant_params((0,), (-1, bsize), padding, slices, amax_shape_for_export)
-            return
-
-        for ax in range(inputs.dim()):
-            bsize, padding, ax_slice = get_axis_quant_params(ax)
-            paddings.append(padding)
-            slices.append(ax_slice)
-            if bsize is not None:
-                reshape_size.extend([math.ceil(inputs.shape[ax] / bsize), bsize])
-                quantize_axis.extend([True, False])
-            else:
-                reshape_size.append(inputs.shape[ax])
-                quantize_axis.append(True)
-        quant_axis = [i for i in range(len(quantize_axis)) if quantize_axis[i]]
-        slices = None if all(s is None for s in slices) else [s or slice(None) for s in slices]
-        if all(p is None for p in paddings):
-            paddings = None
+        padded = torch.Size(n + p for n, _, p in plan)
+        if last_only:
+            bsize = plan[-1][1]
+            axis, view = (0,), (-1, bsize)
         else:
-            new_paddings = []
-            for padding in paddings:
-                if not (new_paddings or padding):
-                    continue
-                new_paddings.extend(padding or (0, 0))
-            paddings = tuple(reversed(new_paddings))
-        set_quant_params(quant_axis, reshape_size, paddings, slices)
+            view, axis = [], []
+            for n, b, p in plan:
+                if b:
+                    axis.append(len(view))
+                    view += [(n + p) // b, b]
+                else:
+                    axis.append(len(view))
+                    view.append(n)
+        self._axis = tuple(axis)
+        if hasattr(self, "_calibrator"):
+            self._calibrator._axis = self._axis
+        self._block_reshape_size = torch.Size(view)
+        self._original_shape = padded
+        if any(p for _, _, p in plan):
+            # F.pad order: (left, right) pairs from the last dim back to the first padded dim
+            first = min(d for d, (_, _, p) in enumerate(plan) if p)
+            pads: list[int] = []
+            for _, _, p in reversed(plan[first:]):
+                pads += [0, p]
+            self._padding = tuple(pads)
+            self._slices = tuple(slice(n) if p else slice(None) for n, _, p in plan)
+        if last_only:
+            self._amax_shape_for_export = (*shape[:-1], -1)
 
     def _process_for_blockquant(self, inputs: torch.Tensor):
-        if hasattr(self, "_padding"):
-            inputs = F.pad(inputs, self._padding, "constant", 0)
+        pads = getattr(self, "_padding", None)
+        if pads is not None:
+            inputs = F.pad(inputs, pads, "constant", 0)
         if inputs.shape != self._original_shape:
             raise ValueError(
                 f"Input shape has changed from {self._original_shape} to {inputs.shape}."
@@ -659,9 +651,8 @@ class TensorQuantizer(nn.Module):
 
     def _reset_to_original_shape(self, outputs: torch.Tensor):
         outputs = outputs.reshape(self._original_shape)
-        if hasattr(self, "_slices"):
-            outputs = outputs[self._slices]
-        return outputs
+        crop = getattr(self, "_slices", None)
+        return outputs if crop is None else outputs[tuple(crop)]
 
     def _block_sizes_to_axis(self, x: torch.Tensor):
         block_sizes = self._block_sizes

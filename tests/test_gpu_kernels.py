@@ -341,7 +341,7 @@ def test_histogram_matches_histc(gpu, bins, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("bins", [64, 2048, 4096, 9000])
+@pytest.mark.parametrize("bins", [64, 2048, 4096, 8192, 9000])
 @pytest.mark.parametrize("skip_zeros", [False, True])
 def test_histogram_16bit_table_path(gpu, dtype, bins, skip_zeros):
     """The per-block bin table of the 16-bit path: zeros, values at / above the range end,
@@ -361,6 +361,23 @@ def test_histogram_16bit_table_path(gpu, dtype, bins, skip_zeros):
     ref = torch.histc(xa[keep], bins=bins, min=0, max=float(hmax))
     counts = torch.zeros(bins, dtype=torch.int32, device=gpu)
     ops().histogram_abs_accumulate(x.to(gpu), hmax.to(gpu).float(), counts, bins, skip_zeros)
+    assert torch.equal(counts.cpu().float(), ref), (counts.cpu().float() - ref).abs().max()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_histogram_pattern_path_many_blocks(gpu, dtype):
+    """The 16-bit pattern histogram over many blocks, a ragged last block chunk and heavy-tailed
+    data (hot bins), vs torch.histc."""
+    g = torch.Generator().manual_seed(7)
+    n = 8 * ((1 << 21) + 3)
+    x = torch.randn(n, generator=g)
+    x[:: 997] *= 16
+    x = x.to(dtype)
+    xa = x.float().abs()
+    hmax = xa.max()
+    ref = torch.histc(xa, bins=2048, min=0, max=float(hmax))
+    counts = torch.zeros(2048, dtype=torch.int32, device=gpu)
+    ops().histogram_abs_accumulate(x.to(gpu), hmax.to(gpu).float(), counts, 2048, False)
     assert torch.equal(counts.cpu().float(), ref), (counts.cpu().float() - ref).abs().max()
 
 
