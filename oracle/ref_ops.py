@@ -410,7 +410,11 @@ def nvfp4_fake_quant_block(x, global_amax, block_size=16):
     blocks = xp.reshape(xp.shape[0], -1, block_size)
     gs = global_amax.float().reshape(()) / torch.tensor(6.0 * 448.0, dtype=torch.float32)
     gs = torch.where(gs > 0, gs, torch.tensor(1e-12, dtype=torch.float32))
-    bmax = blocks.abs().amax(-1, keepdim=True)
+    # tl.max (fp4_kernel_hopper.py:81) is NaN-undefined in Triton; on the hardware it lowers to
+    # max.f32, which skips NaN -- restated as NaN -> 0 (parity for NaN blocks: documented, not
+    # pinned by a reference output).
+    ab = blocks.abs()
+    bmax = torch.where(torch.isnan(ab), torch.zeros_like(ab), ab).amax(-1, keepdim=True)
     s8 = bmax / (torch.tensor(6.0, dtype=torch.float32) * gs)
     s8 = torch.minimum(s8, torch.tensor(448.0))
     q8 = s8.to(torch.float8_e4m3fn).float() * gs

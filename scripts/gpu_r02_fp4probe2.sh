@@ -1,0 +1,5 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 60 ./scripts/probe_fp4_cvt > gpurun_out/fp4probe2.txt 2>&1 || { cat gpurun_out/fp4probe2.txt; exit 10; }
+cat gpurun_out/fp4probe2.txt

@@ -111,6 +111,21 @@ __device__ __forceinline__ float clamp_nan(float v, float lo, float hi) {
 // compute_max_* clamp, tensor_quant_mx.cu:191-193: inf -> FLT_MAX, NaN kept (fmaxf then skips it)
 __device__ __forceinline__ float clamp_flt_max(float a) { return a > 3.402823466e38f ? 3.402823466e38f : a; }
 
+// Running max of magnitudes that skips NaN of either kind, on the bit patterns: a float form
+// (fmaxf, or `a > m ? a : m`, which LLVM folds to v_max_f32 against a constant) lets a
+// signalling NaN -- e.g. a bf16 sNaN pattern widened to fp32 -- through as a quiet NaN, where the
+// reference's block max skips it (tensor_quant_mx.cu:240-294; the oracle maps NaN to 0).
+// m and a are magnitudes (>= 0 or NaN); non-negative floats order like their bit patterns.
+__device__ __forceinline__ uint32_t abs_bits_nonan(float v) {  // |v| bits, NaN -> +0
+  const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
+  return b > 0x7f800000u ? 0u : b;
+}
+__device__ __forceinline__ float max_skip_nan(float m, float a) {
+  const uint32_t mb = __float_as_uint(m), ab = abs_bits_nonan(a);
+  return __uint_as_float(ab > mb ? ab : mb);
+}
+__device__ __forceinline__ float abs_or_zero(float v) { return __uint_as_float(abs_bits_nonan(v)); }
+
 __device__ __forceinline__ float pow2f(int k) {  // 2^k for k in the normal range
   return __uint_as_float((uint32_t)(k + 127) << 23);
 }
@@ -291,6 +306,62 @@ __device__ __forceinline__ void global_scale(float gamax, float lamax, int fmt, 
       (double)convert_fmt(fabsf((float)((double)local_unscale * two_level)), sfmt) / two_level;
   scale = (float)(1.0 / luq);
   unscale = (float)luq;
+}
+
+// ---- native CDNA4 FP4 (E2M1) converts on packed 16-bit pairs ---------------------------------
+// v_cvt_scalef32_pk_fp4_{bf16,f16} converts two 16-bit floats to E2M1 codes of x / 2^e(s) and
+// v_cvt_scalef32_pk_{bf16,f16}_fp4 back to code * 2^e(s) (e(s) = s's exponent field).  Measured
+// on gfx950 (scripts/probe_fp4_cvt*.hip, profiles/r02/fp4_convert_probe.txt): for every bf16 /
+// f16 pattern and every power-of-two scale 2^-130..2^130 they equal the fp32 converts composed
+// with an exact widening / an RNE narrowing, and the fp32 down-convert equals the reference E2M1
+// rounding (tensor_quant_mx.h:104-141: nearest, ties to the even code, saturating at 6) of x / s
+// for every finite value, sign included (-tiny -> -0).  They differ from the reference only on
+// x = -0 (-0 where the reference gives +0) and NaN (signed +-6 where MX gives +6 and NVFP4 -6),
+// which the kernels route to the emulated path.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+
+template <typename T> struct Fp4Native;
+template <> struct Fp4Native<__bf16> {
+  static constexpr uint32_t kInfBits = 0x7f80u;  // |x| patterns above this are NaN
+  static __device__ __forceinline__ uint32_t down(uint32_t w, float s) {
+    return __builtin_amdgcn_cvt_scalef32_pk_fp4_bf16(0u, __builtin_bit_cast(bf16x2_t, w), s, 0);
+  }
+  static __device__ __forceinline__ uint32_t up(uint32_t p, float s) {
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(p, s, 0));
+  }
+};
+template <> struct Fp4Native<_Float16> {
+  static constexpr uint32_t kInfBits = 0x7c00u;
+  static __device__ __forceinline__ uint32_t down(uint32_t w, float s) {
+    return __builtin_amdgcn_cvt_scalef32_pk_fp4_f16(0u, __builtin_bit_cast(f16x2_t, w), s, 0);
+  }
+  static __device__ __forceinline__ uint32_t up(uint32_t p, float s) {
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(p, s, 0));
+  }
+};
+
+// Per-lane scan of 4 packed 16-bit pairs: the largest |x| pattern (NaN patterns sort above inf)
+// and whether any element is -0 (pattern 0x8000), two packed u16 ops per pair.
+struct PairScan {
+  uint32_t max_abs;
+  bool neg_zero;
+};
+__device__ __forceinline__ PairScan scan_pairs(const uint32_t (&w)[4]) {
+  u16x2_t mx = {0, 0}, mn = {0xffff, 0xffff};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(u16x2_t, w[j] & 0x7fff7fffu));
+    mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2_t, w[j] ^ 0x80008000u));
+  }
+  const uint32_t m = mx.x > mx.y ? mx.x : mx.y;
+  return {m, mn.x == 0 || mn.y == 0};
+}
+
+// 16-bit pattern -> fp32 value
+template <typename T> __device__ __forceinline__ float half_bits_to_float(uint32_t b) {
+  return Elem<T>::ld(__builtin_bit_cast(T, (uint16_t)b));
 }
 
 // ---- reductions -----------------------------------------------------------------------------

@@ -39,6 +39,8 @@ int num_cus() {
   return cached[dev];
 }
 
+int env_variant(const char *name, int *cache);
+
 unsigned grid_for(int64_t work_items, int per_block) {
   int64_t blocks = (work_items + per_block - 1) / per_block;
   int64_t cap = (int64_t)num_cus() * 8;
@@ -482,7 +484,7 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   V v = ldg_vec_nt(x + i * N);
   float m = 0.f;
 #pragma unroll
-  for (int j = 0; j < N; ++j) m = fmaxf(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
+  for (int j = 0; j < N; ++j) m = max_skip_nan(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
   m = group_max_f<LPB>(m);
   const int64_t blk = i / LPB;
   float scale, unscale;
@@ -498,9 +500,64 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   stg_vec_nt(y + i * N, v);
 }
 
+// MXFP4 (E2M1 elements, E8M0 scales, no global amax) on 16-bit inputs with the native CDNA4
+// FP4 converts (mtq_device.hpp Fp4Native): per packed pair one down-convert by the block's
+// unscale 2^e and one up-convert by it -- sign(x) * e2m1(|x| * scale) * unscale of
+// tensor_quant_mx.cu:36-55 in 2 instructions per 2 elements instead of ~24 VALU of table
+// emulation.  The block amax comes from packed u16 max of the |x| patterns (NaN detected from
+// the same max); blocks with a NaN, lanes with a -0 and exponents outside [-125, 125] (where the
+// converts' exponent-only scale operand or subnormal results could differ) take the emulated
+// path of mx_vec_kernel, so every element is bit-identical to it.
+template <typename T, int BS>
+__global__ __launch_bounds__(kThreads) void mx_e2m1_native_kernel(const T *__restrict__ x,
+                                                                   T *__restrict__ y,
+                                                                   int64_t nvec) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  static_assert(N == 8 && BS % N == 0, "16-bit elements, block a multiple of the vector");
+  constexpr int LPB = BS / N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i - (threadIdx.x % LPB) >= nvec) return;
+  V v = ldg_vec_nt(x + i * N);
+  uint32_t w[4] = {v.raw.x, v.raw.y, v.raw.z, v.raw.w};
+  const PairScan sc = scan_pairs(w);
+  const uint32_t mb = group_max_u32<LPB>(sc.max_abs);
+  const bool block_nan = mb > Fp4Native<T>::kInfBits;  // uniform over the block's lanes
+  float amax;
+  if (!block_nan) {
+    amax = mb == Fp4Native<T>::kInfBits ? 3.402823466e38f : half_bits_to_float<T>(mb);
+  } else {  // NaN is skipped by the reference's block max, as in mx_vec_kernel
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = max_skip_nan(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
+    amax = group_max_f<LPB>(m);
+  }
+  float scale, unscale;
+  e8m0_scale(amax, 6.0f, scale, unscale);
+  const int ue = (int)((__float_as_uint(unscale) >> 23) & 0xff) - 127;
+  if (!block_nan && !sc.neg_zero && ue >= -125 && ue <= 125) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = Fp4Native<T>::up(Fp4Native<T>::down(w[j], unscale), unscale);
+    v.raw = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, MTQ_E2M1));
+  }
+  stg_vec_nt(y + i * N, v);
+}
+
 template <typename T, int BS>
 void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t stream) {
   const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
+  if constexpr (sizeof(T) == 2) {
+    static int nv = -1;  // MTQ_AMD_FP4_EMULATE=1 forces the table emulation (A/B runs)
+    if (p.fmt == MTQ_E2M1 && p.gamax == nullptr && p.sfmt == MTQ_E8M0 &&
+        env_variant("MTQ_AMD_FP4_EMULATE", &nv) == 0) {
+      mx_e2m1_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec);
+      return;
+    }
+  }
   switch (p.fmt) {
   case MTQ_E2M1: mx_vec_kernel<T, BS, MTQ_E2M1><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
   case MTQ_E4M3: mx_vec_kernel<T, BS, MTQ_E4M3><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
@@ -528,7 +585,7 @@ __global__ __launch_bounds__(kThreads) void mx_scalar_kernel(const T *__restrict
     int64_t col = live ? idx - row * pcols : 0;
     bool real = live && col < cols;
     float v = real ? Elem<T>::ld(x[row * cols + col]) : 0.f;
-    float m = group_max_f<BS>(clamp_flt_max(fabsf(v)));
+    float m = group_max_f<BS>(clamp_flt_max(abs_or_zero(v)));
     if (!real) continue;
     float scale, unscale;
     mx_block_scale(m, row, p, scale, unscale);
@@ -1577,11 +1634,59 @@ __global__ __launch_bounds__(kThreads) void nvfp4_vec_kernel(const T *__restrict
   V v = ldg_vec_nt(x + i * N);
   float m = 0.f;
 #pragma unroll
-  for (int j = 0; j < N; ++j) m = fmaxf(m, fabsf(Elem<T>::ld(v.e[j])));
+  for (int j = 0; j < N; ++j) m = max_skip_nan(m, fabsf(Elem<T>::ld(v.e[j])));
   m = group_max_f<LPB>(m);
   const Nvfp4Block b = nvfp4_block(m, gs);
 #pragma unroll
   for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(nvfp4_qdq(Elem<T>::ld(v.e[j]), b));
+  stg_vec_nt(y + i * N, v);
+}
+
+// NVFP4 on 16-bit inputs with the native E2M1 converts: per element a = RN(x / q) (signed,
+// Markstein as nvfp4_qdq), the pair rounded to E2M1 by one v_cvt_scalef32_pk_fp4_f32 (scale 1)
+// and widened back by one v_cvt_scalef32_pk_f32_fp4, times q.  Symmetric rounding makes the
+// signed form equal to the reference's sign(x) * e2m1(|x| / q) * q except for x = -0 and NaN
+// (mtq_device.hpp Fp4Native): blocks with a NaN and lanes with a -0 take nvfp4_qdq.
+template <typename T, int BS>
+__global__ __launch_bounds__(kThreads) void nvfp4_native_kernel(const T *__restrict__ x,
+                                                                 T *__restrict__ y, int64_t nvec,
+                                                                 const float *__restrict__ gamax) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  static_assert(N == 8 && BS % N == 0, "16-bit elements, block a multiple of the vector");
+  constexpr int LPB = BS / N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i - (threadIdx.x % LPB) >= nvec) return;
+  const float gs = nvfp4_global_scale(gamax);
+  V v = ldg_vec_nt(x + i * N);
+  uint32_t w[4] = {v.raw.x, v.raw.y, v.raw.z, v.raw.w};
+  const PairScan sc = scan_pairs(w);
+  const uint32_t mb = group_max_u32<LPB>(sc.max_abs);
+  const bool block_nan = mb > Fp4Native<T>::kInfBits;
+  float bmax;
+  if (!block_nan) {
+    bmax = half_bits_to_float<T>(mb);
+  } else {  // NaN skipped (max.f32 under the reference's Triton tl.max), as nvfp4_vec_kernel
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = max_skip_nan(m, fabsf(Elem<T>::ld(v.e[j])));
+    bmax = group_max_f<LPB>(m);
+  }
+  const Nvfp4Block b = nvfp4_block(bmax, gs);
+  if (!block_nan && !sc.neg_zero) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a0 = div_rn(Elem<T>::ld(v.e[2 * j]), b.q, b.r);
+      const float a1 = div_rn(Elem<T>::ld(v.e[2 * j + 1]), b.q, b.r);
+      const uint32_t c = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, a0, a1, 1.0f, 0);
+      const auto r = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(c, 1.0f, 0);
+      v.e[2 * j] = Elem<T>::st(r[0] * b.q);
+      v.e[2 * j + 1] = Elem<T>::st(r[1] * b.q);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(nvfp4_qdq(Elem<T>::ld(v.e[j]), b));
+  }
   stg_vec_nt(y + i * N, v);
 }
 
@@ -1601,7 +1706,7 @@ __global__ __launch_bounds__(kThreads) void nvfp4_scalar_kernel(const T *__restr
     const int64_t col = live ? idx - row * pcols : 0;
     const bool real = live && col < cols;
     const float v = real ? Elem<T>::ld(x[row * cols + col]) : 0.f;
-    const float m = group_max_f<BS>(fabsf(v));
+    const float m = group_max_f<BS>(abs_or_zero(v));
     if (!real) continue;
     y[row * cols + col] = Elem<T>::st(nvfp4_qdq(v, nvfp4_block(m, gs)));
   }
@@ -1613,8 +1718,15 @@ int launch_nvfp4(const T *x, T *y, int64_t rows, int64_t cols, const float *gama
   constexpr int N = Vec<T>::N;
   if (cols % BS == 0 && BS % N == 0 && aligned16(x) && aligned16(y)) {
     const int64_t nvec = rows * cols / N;
-    nvfp4_vec_kernel<T, BS><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-        x, y, nvec, gamax);
+    const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
+    if constexpr (sizeof(T) == 2) {
+      static int nv = -1;  // MTQ_AMD_FP4_EMULATE=1 forces the table emulation (A/B runs)
+      if (env_variant("MTQ_AMD_FP4_EMULATE", &nv) == 0) {
+        nvfp4_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec, gamax);
+        return check_launch();
+      }
+    }
+    nvfp4_vec_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec, gamax);
   } else {
     const int64_t pcols = (cols + BS - 1) / BS * BS;
     nvfp4_scalar_kernel<T, BS><<<grid_for(rows * pcols, kThreads), kThreads, 0, stream>>>(

@@ -238,6 +238,50 @@ def test_mx_vs_oracle(gpu, fmt, bs, dtype, cols):
     assert torch.equal(out.cpu().float(), ref.float()) or same_bits(out, ref), mismatch(out, ref)
 
 
+def _all_16bit_patterns(dtype, order):
+    """Every bf16 / f16 bit pattern as one [2048, 32] tensor: "sorted" by magnitude (blocks of
+    like exponents: every E8M0 / E4M3 scale regime incl. subnormal and huge blocks, the NaN / inf
+    patterns together at the end), "shuffled" (NaN, inf, -0 spread over many blocks) or
+    "finite" (shuffled, no NaN / inf)."""
+    bits = torch.arange(65536, dtype=torch.int32).to(torch.int16)
+    x = bits.view(dtype)
+    if order == "sorted":
+        x = x[torch.argsort(x.float().abs().nan_to_num(float("inf")), stable=True)]
+    elif order == "shuffled":
+        x = x[torch.randperm(65536, generator=torch.Generator().manual_seed(3))]
+    else:
+        x = x[torch.isfinite(x.float())]
+        x = x[torch.randperm(x.numel(), generator=torch.Generator().manual_seed(4))]
+        x = x[: x.numel() // 32 * 32]
+    return x.reshape(-1, 32).contiguous()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("order", ["sorted", "shuffled", "finite"])
+@pytest.mark.parametrize("bs", [8, 16, 32])
+def test_mxfp4_native_convert_all_patterns(gpu, dtype, order, bs):
+    """The native-FP4-convert MXFP4 path (mx_e2m1_native_kernel) vs the KAT-pinned oracle on
+    every 16-bit input pattern: -0, NaN of both signs, inf, subnormals, every scale exponent."""
+    x = _all_16bit_patterns(dtype, order)
+    ref = R.fused_amax_convert(x, bs, "E2M1")
+    out = ops().fused_amax_convert(x.to(gpu), bs, R.FORMAT_CODES["E2M1"], R.FORMAT_CODES["E8M0"], None)
+    assert same_bits(out, ref), mismatch(out, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("order", ["sorted", "shuffled", "finite"])
+def test_nvfp4_native_convert_all_patterns(gpu, dtype, order):
+    """The native-FP4-convert NVFP4 path (nvfp4_native_kernel) vs the oracle on every 16-bit
+    input pattern, at several global amax values (block scales from 1e-12 to saturated)."""
+    x = _all_16bit_patterns(dtype, order)
+    fin = x.float().abs()
+    fin = fin[torch.isfinite(fin)]
+    for ga in (fin.amax(), torch.tensor(1.0), torch.tensor(0.0), fin.amax() * 1e-6):
+        ref = R.nvfp4_fake_quant_block(x, ga)
+        out = ops().nvfp4_fake_quant_block(x.to(gpu), ga.to(gpu).float(), 16)
+        assert same_bits(out, ref), (float(ga), mismatch(out, ref))
+
+
 def test_mx_blocksize_error(gpu):
     x = torch.randn(4, 64, device=gpu)
     with pytest.raises(ValueError):
