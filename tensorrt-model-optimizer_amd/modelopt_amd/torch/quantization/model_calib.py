@@ -23,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from modelopt_amd._ext import ops as _ops
-from modelopt_amd.torch.utils.distributed import DistributedProcessGroup
+from modelopt_amd.torch.utils.distributed import DistributedProcessGroup, fixed_order_sum
 
 from .conversion import set_quantizer_by_cfg_context
 from .nn.modules.quant_module import QuantModule
@@ -285,6 +285,7 @@ class _AWQLiteHelper:
         self.num_tokens = 0
         self.module = module
         self.is_enabled = True
+        self.dp_group = None  # set when act_scale is synced over a DP group
 
     def setup(self):
         module = self.module
@@ -449,7 +450,10 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
             if has_nan:
                 h.is_enabled = False
             elif g.is_initialized():
-                dist.all_reduce(h.act_scale, op=dist.ReduceOp.AVG, group=g.group)
+                # reference :1588-1593 all_reduce(AVG): here a fixed-order fp32 sum / world, so
+                # every rank and every run gets the same bits (and gloo, which lacks AVG, works)
+                h.act_scale = fixed_order_sum(h.act_scale, g) / g.world_size()
+                h.dp_group = g
     for _, module in model.named_modules():
         if is_quantized_linear(module) and hasattr(module, "awq_lite") and module.awq_lite.num_cache_steps == 0:
             module.awq_lite.is_enabled = False
@@ -460,6 +464,12 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
     def postprocess(module, name):
         h = module.awq_lite
         if h.is_enabled:
+            if h.dp_group is not None:
+                # Divergence from the reference (which keeps each rank's local losses, so ranks with
+                # different data can pick different alphas and end with different weights): the
+                # per-alpha losses are summed over the DP ranks in rank order, so every rank picks
+                # the alpha a single process over all the data would.
+                h.loss = fixed_order_sum(h.loss, h.dp_group)
             losses = h.loss.tolist()  # one host read per layer
             loss = dict(zip(h.alphas, losses))
             h.best_alpha = min(loss, key=loss.get)

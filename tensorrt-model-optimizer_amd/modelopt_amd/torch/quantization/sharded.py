@@ -18,7 +18,15 @@ Each rank therefore calibrates exactly its own layers' quantizers on the same ac
 single-GPU run would produce, and consecutive batches overlap across stages (batch i on stage r
 while batch i+1 is on stage r-1).  The per-stage amax state is then exchanged with ONE packed
 ``all_reduce(MAX)`` over the world group (every rank ends up with the complete quantizer state,
-as export needs): owners contribute their values, other ranks zeros (amax >= 0).
+as export needs): owners contribute their values, other ranks zeros (amax >= 0).  The same
+exchange carries every quantizer's ``_pre_quant_scale`` (AWQ / SmoothQuant, > 0), and the static
+block weight quantizers are promoted afterwards on every rank (NVFP4's ``_global_amax`` is derived
+from the exchanged amax), so non-owners end with the owners' complete quantizer state.
+
+Inside the context the model's forward returns ``None`` on every rank but the last (the stage
+stops the forward after sending its hidden states): a ``forward_loop`` must not read outputs.
+With the ``gloo`` backend (CPU rehearsal, or several ranks sharing one GPU) device tensors are
+staged through host memory for the point-to-point hand-off and the all-reduce.
 
 Decoder layers must return a tensor (transformers >= 5); models whose parent forward mixes the
 hidden state between layers are not supported (same restriction as layerwise calibration).
@@ -60,6 +68,26 @@ def layer_shard_plan(num_layers: int, rank: int, world: int) -> LayerShardPlan:
     base, extra = divmod(num_layers, world)
     first = rank * base + min(rank, extra)
     return LayerShardPlan(rank, world, first, first + base + (1 if rank < extra else 0), num_layers)
+
+
+def _is_gloo(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
+def _send(t: torch.Tensor, dst: int, group) -> None:
+    """Point-to-point send (RCCL over xGMI; host-staged under gloo, which has no device P2P)."""
+    if t.device.type != "cpu" and _is_gloo(group):
+        t = t.cpu()
+    dist.send(t, dst=dst, group=group)
+
+
+def _recv(buf: torch.Tensor, src: int, group) -> None:
+    if buf.device.type != "cpu" and _is_gloo(group):
+        host = torch.empty(buf.shape, dtype=buf.dtype)
+        dist.recv(host, src=src, group=group)
+        buf.copy_(host)
+    else:
+        dist.recv(buf, src=src, group=group)
 
 
 def _hidden_arg(args, kwargs):
@@ -105,13 +133,13 @@ def layer_sharded_calibration(model: nn.Module, plan: LayerShardPlan, group=None
             if i == plan.first and prev_rank is not None:
                 h, rebuild = _hidden_arg(args, kwargs)
                 buf = torch.empty(h.shape, dtype=h.dtype, device=_device_of(mod, h))
-                dist.recv(buf, src=prev_rank, group=group)
+                _recv(buf, prev_rank, group)
                 args, kwargs = rebuild(buf)
             out = orig(*args, **kwargs)
             if i == plan.last - 1 and next_rank is not None:
                 if not isinstance(out, torch.Tensor):
                     raise TypeError("layer-sharded calibration needs decoder layers that return a tensor")
-                dist.send(out.contiguous(), dst=next_rank, group=group)
+                _send(out.contiguous(), next_rank, group)
                 raise _EarlyStopForwardError()
             return out
 
@@ -161,21 +189,31 @@ def _leaf_quantizers(model: nn.Module):
             yield name, m
 
 
+# per-quantizer tensors the owner's calibration produces and every rank needs (all >= 0, so a
+# MAX all-reduce with zeros from the non-owners returns the owner's values exactly)
+_SYNCED_ATTRS = ("_amax", "_pre_quant_scale")
+
+
 @torch.no_grad()
 def sync_sharded_amax(model: nn.Module, device=None, group=None) -> int:
-    """Give every rank the complete amax state after layer-sharded calibration.
+    """Give every rank the complete quantizer state after layer-sharded calibration.
 
-    Shapes of the owned (real) amax buffers are exchanged as small host objects; the values
-    travel in ONE packed fp32 ``all_reduce(MAX)`` on ``device`` (RCCL on MI355X).  Returns the
-    number of amax entries in the packed buffer.
+    The shapes of the owned (real) ``_amax`` / ``_pre_quant_scale`` buffers are exchanged as small
+    host objects; the values travel in ONE packed fp32 ``all_reduce(MAX)`` on ``device`` (RCCL on
+    MI355X; host-staged under gloo).  Static block weight quantizers are then promoted on every
+    rank.  Returns the number of entries in the packed buffer.
     """
     if not (dist.is_available() and dist.is_initialized()):
         return 0
+    from .model_calib import promote_static_block_weight_quantizers
+
+    mods = dict(_leaf_quantizers(model))
     mine = {}
-    for name, q in _leaf_quantizers(model):
-        a = getattr(q, "_amax", None)
-        if isinstance(a, torch.Tensor) and a.device.type != "meta":
-            mine[name] = (tuple(a.shape), str(a.dtype).replace("torch.", ""))
+    for name, q in mods.items():
+        for attr in _SYNCED_ATTRS:
+            a = q.__dict__.get("_buffers", {}).get(attr, getattr(q, attr, None))
+            if isinstance(a, torch.Tensor) and a.device.type != "meta":
+                mine[(name, attr)] = (tuple(a.shape), str(a.dtype).replace("torch.", ""))
     world = dist.get_world_size(group)
     gathered = [None] * world
     dist.all_gather_object(gathered, mine, group=group)
@@ -183,35 +221,42 @@ def sync_sharded_amax(model: nn.Module, device=None, group=None) -> int:
     for d in gathered:
         for k, v in d.items():
             if k in layout and layout[k] != v:
-                raise RuntimeError(f"amax shape/dtype of {k} differs across ranks: {layout[k]} vs {v}")
+                raise RuntimeError(f"{k[1]} shape/dtype of {k[0]} differs across ranks: {layout[k]} vs {v}")
             layout[k] = v
-    names = sorted(layout)
-    sizes = [int(torch.Size(layout[n][0]).numel()) for n in names]
+    keys = sorted(layout)
+    sizes = [int(torch.Size(layout[k][0]).numel()) for k in keys]
     total = sum(sizes)
     if device is None:
-        device = next((getattr(q, "_amax").device for n, q in _leaf_quantizers(model) if n in mine), None)
+        device = next((getattr(mods[n], a).device for (n, a) in mine), None)
         device = device or torch.device("cuda", torch.cuda.current_device())
     flat = torch.zeros(total, dtype=torch.float32, device=device)
-    mods = dict(_leaf_quantizers(model))
     off = 0
-    for n, k in zip(names, sizes):
-        if n in mine:
-            flat[off : off + k] = mods[n]._amax.detach().reshape(-1).to(device=device, dtype=torch.float32)
-        off += k
-    if dist.get_backend(group) == "gloo" and flat.device.type != "cpu":
+    for k, sz in zip(keys, sizes):
+        if k in mine:
+            flat[off : off + sz] = getattr(mods[k[0]], k[1]).detach().reshape(-1).to(device=device, dtype=torch.float32)
+        off += sz
+    if _is_gloo(group) and flat.device.type != "cpu":
         c = flat.cpu()
         dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
         flat = c.to(device)
     else:
         dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=group)
     off = 0
-    for n, k in zip(names, sizes):
-        shape, dt = layout[n]
-        val = flat[off : off + k].view(shape).to(getattr(torch, dt))
-        q = mods.get(n)
-        if q is not None:
-            if n not in mine and hasattr(q, "_amax"):
+    for k, sz in zip(keys, sizes):
+        (name, attr), (shape, dt) = k, layout[k]
+        val = flat[off : off + sz].view(shape).to(getattr(torch, dt))
+        q = mods.get(name)
+        off += sz
+        if q is None or k in mine:
+            continue
+        if attr == "_amax":
+            if hasattr(q, "_amax"):
                 delattr(q, "_amax")  # a meta placeholder from weight-only calibration
             q.amax = val
-        off += k
+        else:
+            if attr in q._buffers:
+                del q._buffers[attr]
+            q._enable_pre_quant_scale = True
+            q.pre_quant_scale = val
+    promote_static_block_weight_quantizers(model)
     return total

@@ -62,6 +62,28 @@ class DistributedProcessGroup:
         return f"DistributedProcessGroup(group={self.group}, initialized={self.is_initialized()})"
 
 
+def fixed_order_sum(t: torch.Tensor, group: DistributedProcessGroup) -> torch.Tensor:
+    """Sum of ``t`` over the ranks of ``group`` in rank order, fp32, identical on every rank.
+
+    An ``all_reduce(SUM/AVG)`` adds in an order the collective's algorithm picks (ring chunks on
+    RCCL), so the float result can differ across runs and topologies, and gloo has no AVG.  The
+    tensors reduced here are small (an AWQ ``act_scale`` is one [K] vector per linear, the losses
+    11 floats): gather them all and add ``((t_0 + t_1) + t_2) + ...`` on every rank instead.
+    Host-staged under gloo when ``t`` lives on a device."""
+    if not group.is_initialized():
+        return t
+    dev = t.device
+    x = t.detach().to(torch.float32)
+    if dist.get_backend(group.group) == "gloo" and x.device.type != "cpu":
+        x = x.cpu()
+    parts = [torch.empty_like(x) for _ in range(group.world_size())]
+    dist.all_gather(parts, x.contiguous(), group=group.group)
+    acc = parts[0].clone()
+    for p in parts[1:]:
+        acc += p
+    return acc.to(dev)
+
+
 class ParallelState:
     """Data / tensor / expert parallel groups of a module (reference :441-466)."""
 

@@ -68,3 +68,46 @@ def test_packed_amax_sync_world2():
     for rank, n, ok in res:
         assert n == 1, "one collective for all quantizers"
         assert ok, f"rank {rank}: packed sync != per-quantizer MAX all-reduce"
+
+
+def _sum_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from modelopt_amd.torch.utils.distributed import DistributedProcessGroup, fixed_order_sum
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(100 + rank)
+        t = torch.randn(4096, generator=g) * 10 ** torch.randint(-6, 6, (4096,), generator=g).float()
+        got = fixed_order_sum(t, DistributedProcessGroup(None))
+        # the same rank-order sum computed from every rank's tensor regenerated locally
+        parts = []
+        for r in range(world):
+            gr = torch.Generator().manual_seed(100 + r)
+            parts.append(torch.randn(4096, generator=gr) * 10 ** torch.randint(-6, 6, (4096,), generator=gr).float())
+        want = parts[0].clone()
+        for p in parts[1:]:
+            want += p
+        q.put((rank, bool(torch.equal(got, want)), got.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_fixed_order_sum_world3_identical_bits():
+    """utils.distributed.fixed_order_sum (AWQ act_scale / loss DP reduction, replacing the
+    reference's all_reduce(AVG), model_calib.py:1588-1593): the rank-order fp32 sum on every rank,
+    bit-identical across ranks (gloo has no AVG; RCCL's ring order is not fixed)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sum_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=30)
+    assert all(ok for _, ok, _ in res)
+    assert len({b for _, _, b in res}) == 1
