@@ -168,15 +168,35 @@ def kernel_suite(ops, xs, steps, warmup):
     return res
 
 
-def cpu_baseline(target_s: float = 10.0):
-    """Oracle restatement of the reference eager FP8 block path, timed on host cores."""
-    from oracle import ref_ops as R  # test infrastructure: the checker / CPU baseline only
+def host_cpu_info():
+    """Physical cores of the host (unique (package, core) pairs in /proc/cpuinfo), the CPUs this
+    process may run on, and torch's intra-op thread count."""
+    phys = set()
+    try:
+        pkg = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k = k.strip()
+            if k == "physical id":
+                pkg = v.strip()
+            elif k == "core id":
+                core = v.strip()
+            elif not k and pkg is not None:
+                phys.add((pkg, core))
+                pkg = core = None
+        if pkg is not None:
+            phys.add((pkg, core))
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count()
+    return {"host_physical_cores": len(phys) or None, "process_cpus": allowed,
+            "torch_threads": torch.get_num_threads()}
 
-    rows = 8192  # bounded sample: [8192, 4096] bf16 = 33.5 M elements per pass
-    g = torch.Generator().manual_seed(1234)
-    x = torch.randn(rows, HIDDEN, generator=g).to(torch.bfloat16)
-    xb = x.view(-1, BLOCK)
-    amax = xb.abs().amax(dim=1, keepdim=True).float()
+
+def _time_fp8_eager(R, xb, amax, target_s):
     R.fp8_eager(xb, amax)  # warm-up
     passes, t0 = 0, time.perf_counter()
     while True:
@@ -184,15 +204,42 @@ def cpu_baseline(target_s: float = 10.0):
         passes += 1
         el = time.perf_counter() - t0
         if el >= target_s or passes >= 200:
-            break
-    elems = passes * x.numel()
+            return passes, el
+
+
+def cpu_baseline(target_s: float = 10.0):
+    """Oracle restatement of the reference eager FP8 block path, timed on host cores: all the
+    threads torch uses here (the box's per-job CPU share) and one thread."""
+    from oracle import ref_ops as R  # test infrastructure: the checker / CPU baseline only
+
+    rows = 8192  # bounded sample: [8192, 4096] bf16 = 33.5 M elements per pass
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(rows, HIDDEN, generator=g).to(torch.bfloat16)
+    xb = x.view(-1, BLOCK)
+    amax = xb.abs().amax(dim=1, keepdim=True).float()
+    info = host_cpu_info()
+    passes, el = _time_fp8_eager(R, xb, amax, target_s)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        xs1 = xb[: 1024 * HIDDEN // BLOCK]
+        p1, el1 = _time_fp8_eager(R, xs1, amax[: xs1.shape[0]], target_s / 2)
+    finally:
+        torch.set_num_threads(nt)
     return {
-        "value": round(elems / el / 1e9, 4),
+        "value": round(passes * x.numel() / el / 1e9, 4),
         "unit": "G-elem/s",
-        "cores": torch.get_num_threads(),
+        "cores": nt,
         "kind": "port",
         "sample": f"{passes} passes of FP8 e4m3 static block-128 fake-quant (oracle fp8_eager, the "
-        f"reference _fp8_eager ATen sequence) over bf16 [{rows}, {HIDDEN}], {el:.1f} s",
+        f"reference _fp8_eager ATen sequence) over bf16 [{rows}, {HIDDEN}], {el:.1f} s, {nt} threads",
+        "one_thread": {
+            "value": round(p1 * xs1.numel() / el1 / 1e9, 4),
+            "unit": "G-elem/s",
+            "cores": 1,
+            "sample": f"{p1} passes over bf16 [1024, {HIDDEN}], {el1:.1f} s",
+        },
+        **info,
     }
 
 
@@ -271,6 +318,7 @@ def main():
     ap.add_argument("--no-suite", action="store_true", help="skip the secondary kernel table")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-ptq", action="store_true", help="skip the Llama-3-8B FP8 PTQ wall-clock")
+    ap.add_argument("--no-c3", action="store_true", help="skip the Llama-3-8B INT4 AWQ-lite PTQ (C3)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
@@ -343,6 +391,16 @@ def main():
         res["ptq_wall_clock_s"] = round(_max_over_ranks(dist, res["ptq_wall_clock_s"]), 3)
         res["calib_tokens_per_s"] = round(512 * 512 / res["ptq_wall_clock_s"], 1)
         out["ptq"] = res
+        if not args.no_c3:
+            # C3: INT4 AWQ-lite (block 128) on the same model and calibration set
+            print("bench: C3 INT4_AWQ_CFG PTQ ...", file=sys.stderr, flush=True)
+            _barrier(dist)
+            with contextlib.redirect_stdout(sys.stderr):
+                r3 = ptq_llama.run(samples=512, seq=512, rank=rank, world=world, baseline=False,
+                                   config="INT4_AWQ_CFG")
+            r3["ptq_wall_clock_s"] = round(_max_over_ranks(dist, r3["ptq_wall_clock_s"]), 3)
+            r3["calib_tokens_per_s"] = round(512 * 512 / r3["ptq_wall_clock_s"], 1)
+            out["ptq_c3"] = r3
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_ptq:

@@ -256,6 +256,25 @@ int mtq_awq_clip_search(const void *w, const float *x, int64_t co, int64_t cols,
                         int n_shrinks, int block, int num_bits, int is_unsigned, int narrow_range,
                         float *loss, int accumulate, hipStream_t stream);
 
+/* ---- host (CPU) kernels: the reference's "cpu" op registration ---------------------------
+ * The reference registers tensorrt::quantize_op for ["cpu", "cuda"] (tensor_quant.py:252-256)
+ * and runs `_tensor_quant` (:607-645), `_fp8_eager` (:46-59) and `reduce_amax`
+ * (utils/core_utils.py:146-183) as eager ATen on CPU tensors.  These are the same arithmetic
+ * on host memory (x, y, amax, out are host pointers; amax is fp32 with axis_size elements,
+ * channel of element i = (i / inner) % axis_size, axis_size 1 = per tensor), multi-threaded
+ * with `nthreads` std::threads (0 = all hardware threads), bit-exact with the ATen sequences.
+ *  mtq_cpu_fake_tensor_quant: INT-n qdq, as mtq_fake_tensor_quant(_with_axis).
+ *  mtq_cpu_fake_e4m3fy:       FP8 qdq, as mtq_fake_e4m3fy(_with_axis); amax NULL = the plain
+ *                             e4m3 cast round trip (mtq_e4m3_cast).
+ *  mtq_cpu_reduce_amax:       as mtq_reduce_amax (accumulating, NaN-propagating). */
+int mtq_cpu_fake_tensor_quant(const void *x, void *y, int64_t n, int dtype, const float *amax,
+                              int64_t axis_size, int64_t inner, int num_bits, int is_unsigned,
+                              int narrow_range, int nthreads);
+int mtq_cpu_fake_e4m3fy(const void *x, void *y, int64_t n, int dtype, const float *amax,
+                        int64_t axis_size, int64_t inner, int nthreads);
+int mtq_cpu_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtype, float *out,
+                        int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,14 +5,18 @@
 // modelopt/torch/quantization/tensor_quant.py:222-276) and of its pybind extension modules
 // (modelopt_cuda_ext, tensor_quant.cpp:63-76; modelopt_cuda_ext_fp8,
 // tensor_quant_gpu_fp8.cu:109-114; modelopt_cuda_ext_mx, tensor_quant_mx.cu:393-411), plus
-// the calibration reductions.  Only the device ("CUDA" dispatch key = HIP on ROCm) and Meta
-// keys are implemented: there is no CPU compute path in the product, a CPU tensor raises.
-// Every kernel runs on the caller's current HIP stream; nothing here synchronises.
+// the calibration reductions, on the device ("CUDA" dispatch key = HIP on ROCm) and Meta keys.
+// The reference also registers "cpu" (tensor_quant.py:252-256): the INT / FP8 qdq ops and the
+// amax reduction have CPU implementations here too, on the product's own host kernels
+// (mtq_cpu_*, csrc/mtq_cpu.cpp); every other op raises on a CPU tensor.
+// Every device kernel runs on the caller's current HIP stream; nothing here synchronises.
 #include <torch/library.h>
 #include <ATen/ATen.h>
+#include <ATen/Parallel.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -49,6 +53,13 @@ void check_status(int st, const char *what) {
 void check_device(const at::Tensor &t, const char *name) {
   TORCH_CHECK(t.is_cuda(), "modelopt_amd: ", name,
               " must be on a ROCm (HIP) device; the MI355X-native path has no CPU kernels");
+}
+
+int cpu_threads() { return std::max(1, (int)at::get_num_threads()); }
+
+// fp32 amax on the host for the CPU kernels (reference: amax.float())
+at::Tensor cpu_amax(const at::Tensor &amax) {
+  return amax.to(at::kCPU).to(at::kFloat).contiguous();
 }
 
 int checked_dtype(const at::Tensor &t, const char *name) {
@@ -126,6 +137,28 @@ void int_qdq_into(const at::Tensor &x, at::Tensor &y, const at::Tensor &amax_in,
                   bool is_unsigned, bool narrow_range);
 void int_qdq_into(const at::Tensor &x, at::Tensor &y, const at::Tensor &amax_in, int64_t num_bits,
                   bool is_unsigned, bool narrow_range) {
+  if (x.is_cpu()) {
+    at::Tensor xc = x.contiguous();
+    at::Tensor amax = cpu_amax(amax_in);
+    AxisMap m = axis_map(xc, amax);
+    if (!m.adjacent) {
+      y.copy_(permuted(xc, amax, [&](const at::Tensor &xp, const at::Tensor &ap) {
+        at::Tensor yp = at::empty_like(xp);
+        int_qdq_into(xp, yp, ap, num_bits, is_unsigned, narrow_range);
+        return yp;
+      }));
+      return;
+    }
+    at::Tensor yc = y.is_contiguous() ? y : at::empty_like(xc);
+    check_status(mtq_cpu_fake_tensor_quant(xc.data_ptr(), yc.data_ptr(), xc.numel(),
+                                           checked_dtype(xc, "inputs"), amax.data_ptr<float>(),
+                                           m.per_tensor ? 1 : m.axis_size,
+                                           m.per_tensor ? 1 : m.inner, (int)num_bits, is_unsigned,
+                                           narrow_range, cpu_threads()),
+                 "fake_tensor_quant (cpu)");
+    if (!yc.is_same(y)) y.copy_(yc);
+    return;
+  }
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
   at::Tensor amax = amax_operand(amax_in, x);
@@ -175,6 +208,16 @@ at::Tensor fake_tensor_quant_with_axis(const at::Tensor &inputs, const at::Tenso
   const int64_t ax = axis < 0 ? axis + x.dim() : axis;
   TORCH_CHECK(ax >= 0 && ax < x.dim(), "axis out of range");
   TORCH_CHECK(amax.numel() == x.size(ax), "amax must have size(axis) elements");
+  if (x.is_cpu()) {
+    at::Tensor a = cpu_amax(amax);
+    at::Tensor y = at::empty_like(x);
+    check_status(mtq_cpu_fake_tensor_quant(x.data_ptr(), y.data_ptr(), x.numel(),
+                                           checked_dtype(x, "inputs"), a.data_ptr<float>(),
+                                           x.size(ax), x.stride(ax), (int)num_bits, is_unsigned,
+                                           narrow_range, cpu_threads()),
+                 "fake_tensor_quant_with_axis (cpu)");
+    return y;
+  }
   check_device(x, "inputs");
   at::Tensor a = amax_operand(amax, x);
   at::Tensor y = at::empty_like(x);
@@ -197,6 +240,21 @@ bool storage_order_ok(const at::Tensor &t, const at::Tensor &amax) {
 }
 
 at::Tensor fp8_qdq(const at::Tensor &inputs, const at::Tensor &amax_in) {
+  if (inputs.is_cpu()) {
+    at::Tensor x = inputs.contiguous();
+    at::Tensor amax = cpu_amax(amax_in);
+    AxisMap m = axis_map(x, amax);
+    if (!m.adjacent) return permuted(x, amax, [](const at::Tensor &xp, const at::Tensor &ap) {
+      return fp8_qdq(xp, ap);
+    });
+    at::Tensor y = at::empty_like(x);
+    check_status(mtq_cpu_fake_e4m3fy(x.data_ptr(), y.data_ptr(), x.numel(),
+                                     checked_dtype(x, "inputs"), amax.data_ptr<float>(),
+                                     m.per_tensor ? 1 : m.axis_size, m.per_tensor ? 1 : m.inner,
+                                     cpu_threads()),
+                 "fake_e4m3fy (cpu)");
+    return y;
+  }
   at::Tensor x = storage_order_ok(inputs, amax_in) ? inputs : inputs.contiguous();
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
@@ -229,6 +287,15 @@ at::Tensor fake_e4m3fy_with_axis(const at::Tensor &inputs, const at::Tensor &ama
   const int64_t ax = axis < 0 ? axis + x.dim() : axis;
   TORCH_CHECK(ax >= 0 && ax < x.dim(), "axis out of range");
   TORCH_CHECK(amax.numel() == x.size(ax), "amax must have size(axis) elements");
+  if (x.is_cpu()) {
+    at::Tensor a = cpu_amax(amax);
+    at::Tensor y = at::empty_like(x);
+    check_status(mtq_cpu_fake_e4m3fy(x.data_ptr(), y.data_ptr(), x.numel(),
+                                     checked_dtype(x, "inputs"), a.data_ptr<float>(), x.size(ax),
+                                     x.stride(ax), cpu_threads()),
+                 "fake_e4m3fy_with_axis (cpu)");
+    return y;
+  }
   check_device(x, "inputs");
   at::Tensor a = amax_operand(amax, x);
   at::Tensor y = at::empty_like(x);
@@ -244,6 +311,13 @@ at::Tensor fake_e4m3fy_with_axis(const at::Tensor &inputs, const at::Tensor &ama
 // plain e4m3 cast round trip (`_fp8_eager` with amax=None, tensor_quant.py:55-59).
 at::Tensor e4m3_cast(const at::Tensor &inputs) {
   at::Tensor x = inputs.contiguous();
+  if (x.is_cpu()) {
+    at::Tensor y = at::empty_like(x);
+    check_status(mtq_cpu_fake_e4m3fy(x.data_ptr(), y.data_ptr(), x.numel(),
+                                     checked_dtype(x, "inputs"), nullptr, 1, 1, cpu_threads()),
+                 "e4m3_cast (cpu)");
+    return y;
+  }
   check_device(x, "inputs");
   at::Tensor y = at::empty_like(x);
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
@@ -284,10 +358,17 @@ at::Tensor fused_amax_convert(const at::Tensor &inputs, int64_t block_size, int6
 // out (fp32, contiguous, K elements) = max(out, max_{p,q} |x[p,k,q]|)
 void amax_accumulate(const at::Tensor &inputs, at::Tensor out, int64_t P, int64_t K, int64_t Q) {
   at::Tensor x = inputs.contiguous();
-  check_device(x, "inputs");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == K,
               "amax_accumulate: out must be a contiguous fp32 tensor with K elements");
   TORCH_CHECK(P * K * Q == x.numel(), "amax_accumulate: view [P,K,Q] does not match numel");
+  if (x.is_cpu()) {
+    TORCH_CHECK(out.is_cpu(), "amax_accumulate: out must be on the input's device");
+    check_status(mtq_cpu_reduce_amax(x.data_ptr(), P, K, Q, checked_dtype(x, "inputs"),
+                                     out.data_ptr<float>(), cpu_threads()),
+                 "reduce_amax (cpu)");
+    return;
+  }
+  check_device(x, "inputs");
   int dt = checked_dtype(x, "inputs");
   at::Tensor xx = x;
   if (dt == MTQ_F64) {  // exactness for doubles is lost in fp32; upcast path not provided
@@ -739,6 +820,18 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("nvfp4_fp8_scale_sweep", &nvfp4_fp8_scale_sweep);
   m.impl("mse_sweep", &mse_sweep);
   m.impl("awq_clip_search", &awq_clip_search);
+}
+
+// the reference's "cpu" registration (tensor_quant.py:252-256), on the host kernels
+TORCH_LIBRARY_IMPL(modelopt_amd, CPU, m) {
+  m.impl("quantize_op", &quantize_op);
+  m.impl("fake_tensor_quant", &fake_tensor_quant);
+  m.impl("fake_tensor_quant_", &fake_tensor_quant_);
+  m.impl("fake_tensor_quant_with_axis", &fake_tensor_quant_with_axis);
+  m.impl("fake_e4m3fy", &fake_e4m3fy);
+  m.impl("fake_e4m3fy_with_axis", &fake_e4m3fy_with_axis);
+  m.impl("e4m3_cast", &e4m3_cast);
+  m.impl("amax_accumulate", &amax_accumulate);
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, Meta, m) {

@@ -11,7 +11,10 @@ exact max, so order and fusion cannot change it); the differences are where the 
 * a second ``collect`` of the *same* data at the same version -- the same tensor object, or the
   same view (offset/shape/stride) of the same live base tensor (the weight of a QuantLinear, or
   one expert's slice of a fused [E, N, K] expert weight, during ``forward_loop``, which the
-  reference re-reduces on every batch) -- is skipped: max(a, a) = a.
+  reference re-reduces on every batch) -- is skipped: max(a, a) = a.  The skip holds only
+  within one collection epoch (``enable_stats_collection`` opens a new one), because writes
+  through ``.data`` (weight folding between calibration passes) do not bump ``_version``;
+  inference tensors (no version counter) are never skipped.
 """
 
 from __future__ import annotations
@@ -28,6 +31,16 @@ __all__ = ["MaxCalibrator"]
 # The last tensor reduced by a calibrator: (weakref to its base, (view key, _version, reduce
 # axes), weakref to the calibrator, its per-call amax buffer or None).  See _accumulate.
 _SHARED = None
+# Collection epoch: bumped by ``new_collect_epoch`` (called from ``enable_stats_collection``).
+_EPOCH = 0
+
+
+def new_collect_epoch() -> None:
+    """Forget every calibrator's "same tensor as last collect" key (``.data`` writes between
+    calibration passes do not bump ``_version``, so a key may not outlive its pass)."""
+    global _EPOCH, _SHARED
+    _EPOCH += 1
+    _SHARED = None
 
 
 class MaxCalibrator(_Calibrator):
@@ -59,7 +72,9 @@ class MaxCalibrator(_Calibrator):
     def _same_as_last(self, x) -> bool:
         if self._last is None:
             return False
-        ref, key, ver = self._last
+        ref, key, ver, epoch = self._last
+        if epoch != _EPOCH or x.is_inference():
+            return False
         base, k = self._view_key(x)
         return ref() is base and k == key and x._version == ver
 
@@ -84,12 +99,14 @@ class MaxCalibrator(_Calibrator):
         elif list(keep_shape) != list(self._out_shape):
             raise RuntimeError("amax shape changed!")
         self._validated = False
-        try:
-            base, key = self._view_key(x)
-            self._last = (weakref.ref(base), key, x._version)
-        except TypeError:
-            base = None
-            self._last = None
+        base = None
+        self._last = None
+        if not x.is_inference():  # inference tensors have no version counter
+            try:
+                base, key = self._view_key(x)
+                self._last = (weakref.ref(base), key, x._version, _EPOCH)
+            except TypeError:
+                base = None
         self._accumulate(x, reduce_axis, base)
         if self._track_amax:
             self._amaxs.append(quant_utils.reduce_amax(x, axis=reduce_axis).cpu().numpy())

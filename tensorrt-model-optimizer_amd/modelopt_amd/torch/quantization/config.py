@@ -331,7 +331,9 @@ class QuantizeAlgorithmConfig(_Config):
 
     model_config = ConfigDict(extra="allow", validate_assignment=True, arbitrary_types_allowed=True)
     method: str | None = None
-    moe_calib_experts_ratio: float | None = None
+    # fraction of experts every token is routed to during calibration forwards (reference
+    # config.py:793-803; 0 < r <= 1)
+    moe_calib_experts_ratio: float | None = Field(default=None, gt=0.0, le=1.0)
     layerwise: Any = None
 
 

@@ -48,6 +48,9 @@ ForwardLoop = Callable[[nn.Module], None]
 
 def enable_stats_collection(model: nn.Module):
     """Quant off, calib on for every enabled quantizer (reference :1128-1141)."""
+    from .calib.max import new_collect_epoch
+
+    new_collect_epoch()
     for _, module in model.named_modules():
         if isinstance(module, TensorQuantizer) and not module._disabled:
             if module._use_constant_amax or module._constant_amax is not None:

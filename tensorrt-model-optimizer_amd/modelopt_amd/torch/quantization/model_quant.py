@@ -43,7 +43,14 @@ def _apply_algorithm(model, algo_cfg, forward_loop):
         return
     kwargs = algo_cfg.model_dump()
     method = kwargs.pop("method")
-    kwargs.pop("moe_calib_experts_ratio", None)
+    ratio = kwargs.pop("moe_calib_experts_ratio", None)
+    if ratio is not None:
+        # reference mode.py:240-247: set on every sparse sequential MoE block; transformers-5
+        # fused-expert blocks have no such wrapper there either, so the ratio has no effect on them
+        assert isinstance(ratio, (int, float)) and 0 < ratio <= 1, f"Invalid moe_calib_experts_ratio {ratio!r}"
+        for module in model.modules():
+            if hasattr(module, "_moe_calib_experts_ratio"):
+                module._moe_calib_experts_ratio = ratio
     layerwise = kwargs.pop("layerwise", None) or {}
     if layerwise is True:
         layerwise = {"enable": True}

@@ -67,6 +67,8 @@ def _fused_forward(mod, input):
     weight = mod._parameters.get("weight")
     if weight is None or weight.dtype != input.dtype or weight.dim() != 2:
         return None
+    if not weight.is_contiguous() or weight.data_ptr() % 16:
+        return None  # a view into a fused / tied parameter: the kernel streams 16-byte vectors
     n, k = weight.shape
     if input.shape[-1] != k or k % 32 or n % 16 or input.numel() // max(k, 1) > _FUSED_MAX_ROWS:
         return None

@@ -103,6 +103,142 @@ class _QuantFusedExperts(QuantModule):
                 self._fold_weight_quantizer(q, (w,), keep_attrs)
 
 
+def _has_num_experts(obj) -> bool:
+    return hasattr(obj, "num_experts") or hasattr(obj, "n_routed_experts")
+
+
+def _num_experts(*objs) -> int:
+    for obj in objs:
+        for attr in ("num_experts", "n_routed_experts"):
+            n = getattr(obj, attr, None) if obj is not None else None
+            if n:
+                return int(n)
+    return 0
+
+
+class _QuantSparseSequentialMoe(QuantModule):
+    """MoE block whose ``experts`` is iterable (one module per expert, each expert's linears are
+    QuantLinear on their own) -- reference plugins/huggingface.py:623-750.
+
+    With ``_moe_calib_experts_ratio`` set (``algorithm={"moe_calib_experts_ratio": r}``), every
+    calibration forward first routes the tokens to ``max(top_k, round(E * r))`` experts (output
+    discarded, so more experts see tokens and get activation amax), then runs the original
+    ``top_k`` forward; tokens routed per expert are counted in ``expert_token_count`` while
+    ``r < 1``.  Without it the forward is the original one."""
+
+    def _setup(self):
+        self._moe_calib_experts_ratio = None
+        self._token_counting_initialized = False
+        self._count_expert_tokens = False
+
+    def _init_token_counting(self):
+        self._token_counting_initialized = True
+        n = _num_experts(getattr(self, "gate", None), self, getattr(self, "experts", None))
+        if n == 0:
+            import warnings
+
+            warnings.warn(f"{type(self).__name__}: could not resolve num_experts; expert routing is not tracked.")
+            return
+        dev = next(self.parameters()).device
+        self.register_buffer("expert_token_count", torch.zeros(n, dtype=torch.long, device=dev), persistent=False)
+        if hasattr(self, "gate"):
+            self.gate.register_forward_hook(self._gate_forward_hook)
+
+    def _gate_forward_hook(self, module, input, output):
+        if not self._count_expert_tokens or not hasattr(self, "expert_token_count"):
+            return
+        with torch.no_grad():
+            if isinstance(output, tuple) and len(output) >= 3:  # transformers-5 TopKRouter
+                indices = output[2]
+            else:
+                logits = output[0] if isinstance(output, tuple) else output
+                top_k = self.gate.top_k if hasattr(self.gate, "top_k") else self.top_k
+                indices = torch.topk(logits.float(), top_k, dim=-1)[1]
+            counts = torch.bincount(indices.reshape(-1), minlength=self.expert_token_count.shape[0])
+            self.expert_token_count += counts.to(self.expert_token_count.device)
+
+    def _top_k_owner(self):
+        if hasattr(self, "gate") and hasattr(self.gate, "top_k"):
+            return self.gate
+        return self
+
+    def forward(self, hidden_states, *args, **kwargs):
+        fwd = self._original_cls.forward
+        if self._moe_calib_experts_ratio is None:
+            return fwd(self, hidden_states, *args, **kwargs)
+        is_calib = any(getattr(m, "_if_calib", False) for m in self.experts.modules())
+        if is_calib:
+            self._count_expert_tokens = self._moe_calib_experts_ratio < 1.0
+            if self._count_expert_tokens and not self._token_counting_initialized:
+                self._init_token_counting()
+            owner = self._top_k_owner()
+            n = _num_experts(getattr(self, "gate", None), self) or len(self.experts)
+            original = owner.top_k
+            owner.top_k = max(original, round(n * self._moe_calib_experts_ratio))
+            try:
+                fwd(self, hidden_states, *args, **kwargs)
+            finally:
+                owner.top_k = original
+            self._count_expert_tokens = False
+        out = fwd(self, hidden_states, *args, **kwargs)
+        self._count_expert_tokens = False
+        return out
+
+    def layer_sync_moe_local_experts_amax(self, sync_weight_amax=False):
+        """Element-wise max of every expert's input (and optionally weight) amax, written back
+        to all experts; experts that saw no token get a weight-only max calibration (reference
+        core_utils.py:710-750).  Skipped with ``_moe_calib_experts_ratio`` set."""
+        if self._moe_calib_experts_ratio is not None:
+            return
+        from ..model_calib import max_calibrate
+
+        amax: dict = {}
+        for expert in self.experts:
+            for name, m in expert.named_modules():
+                if not isinstance(m, TensorQuantizer) or m.amax is None:
+                    continue
+                if "input_quantizer" in name or (sync_weight_amax and "weight_quantizer" in name):
+                    a = m.amax.detach().clone()
+                    amax[name] = a if name not in amax else torch.maximum(amax[name], a)
+        for expert in self.experts:
+            for name, m in expert.named_modules():
+                if isinstance(m, TensorQuantizer) and name in amax:
+                    m.amax = amax[name].detach().clone()
+        for expert in self.experts:
+            for name, m in expert.named_modules():
+                if name.endswith("weight_quantizer") and m.is_enabled and m.amax is None:
+                    w = expert.state_dict().get(name.replace("weight_quantizer", "weight"))
+                    if w is not None:
+                        max_calibrate(m, lambda q, w=w: q(w), distributed_sync=False)
+
+
+def _is_sparse_sequential_moe_block(module) -> bool:
+    """``gate`` (top_k + num_experts) + iterable ``experts`` (reference :1592-1622)."""
+    if not hasattr(module, "experts") or not hasattr(module.experts, "__iter__"):
+        return False
+    gate = getattr(module, "gate", None)
+    if gate is not None and hasattr(gate, "top_k") and _has_num_experts(gate):
+        return True
+    if hasattr(module, "top_k"):
+        if not _has_num_experts(module) and hasattr(module.experts, "__len__"):
+            module.num_experts = len(module.experts)
+        return _has_num_experts(module)
+    return False
+
+
+@register_on_the_fly
+def register_sparse_moe_on_the_fly(model):
+    """Register every sparse sequential MoE block type of ``model`` (reference :1625-1649)."""
+    seen = set()
+    for _, module in model.named_modules():
+        t = type(module)
+        if t in seen or t in QuantModuleRegistry:
+            continue
+        seen.add(t)
+        if _is_sparse_sequential_moe_block(module):
+            QuantModuleRegistry.register({t: f"hf.{t.__name__}"})(_QuantSparseSequentialMoe)
+
+
 def _is_fused_experts_module(module) -> bool:
     return _fused_experts_wrapper_class(module) is not None
 

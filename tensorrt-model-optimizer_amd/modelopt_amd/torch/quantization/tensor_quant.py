@@ -3,8 +3,10 @@
 The autograd Functions keep the reference's names, argument order and straight-through-estimator
 backward (tensor_quant.py:279-568); their forward calls ``torch.ops.modelopt_amd.*`` (HIP kernels
 behind include/mtq_amd.h).  ``quantize_op`` / ``dynamic_block_quantize_op`` carry the reference's
-torch.library schemas (tensor_quant.py:222-276) in the ``modelopt_amd`` namespace.  There is no
-ATen fallback: a CPU tensor or a missing extension raises.
+torch.library schemas (tensor_quant.py:222-276) in the ``modelopt_amd`` namespace and, as aliases,
+under the reference's own ``tensorrt::`` names.  There is no ATen fallback: a missing extension
+raises; CPU tensors run the product's host kernels for INT / FP8 (the reference's "cpu" key)
+and raise for the other formats.
 """
 
 from __future__ import annotations
@@ -71,6 +73,57 @@ def dynamic_block_quantize_op(
     return ops.dynamic_block_quantize_op(
         input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
     )
+
+
+def _register_reference_op_names() -> bool:
+    """Register the reference's own op names -- ``tensorrt::quantize_op``,
+    ``tensorrt::dynamic_block_quantize_op`` and its ``.overload`` (None amax), schemas of
+    tensor_quant.py:222-237 -- on the CUDA (= HIP), CPU and Meta keys, so code that calls
+    ``torch.ops.tensorrt.*`` directly (or a torch.export graph holding them) runs on these
+    kernels.  The ``.overload`` computes the quantization (the reference's implementation of it
+    returns ``torch.empty_like(input)``, tensor_quant.py:240-249, uninitialised memory).  When the
+    reference package already defined the namespace in this process, its registration stays and
+    nothing is replaced (returns False)."""
+    try:
+        lib = torch.library.Library("tensorrt", "FRAGMENT")
+        lib.define(
+            "quantize_op(Tensor input, Tensor amax, int num_bits, int exponent_bits, "
+            "bool unsigned, bool narrow_range) -> Tensor"
+        )
+        lib.define(
+            "dynamic_block_quantize_op(Tensor input, int block_size, Tensor amax, int num_bits, "
+            "int exponent_bits, int scale_num_bits, int scale_exponent_bits) -> Tensor"
+        )
+        lib.define(
+            "dynamic_block_quantize_op.overload(Tensor input, int block_size, None amax, int num_bits, "
+            "int exponent_bits, int scale_num_bits, int scale_exponent_bits) -> Tensor"
+        )
+    except RuntimeError:
+        return False
+
+    def _q(input, amax, num_bits, exponent_bits, unsigned, narrow_range):
+        return quantize_op(input, amax, num_bits, exponent_bits, unsigned, narrow_range)
+
+    def _d(input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits):
+        return dynamic_block_quantize_op(
+            input, block_size, amax, num_bits, exponent_bits, scale_num_bits, scale_exponent_bits
+        )
+
+    def _fake(input, *args):
+        return torch.empty_like(input)
+
+    for key in ("CUDA", "CPU"):
+        lib.impl("quantize_op", _q, key)
+        lib.impl("dynamic_block_quantize_op", _d, key)
+        lib.impl("dynamic_block_quantize_op.overload", _d, key)
+    for name in ("quantize_op", "dynamic_block_quantize_op", "dynamic_block_quantize_op.overload"):
+        lib.impl(name, _fake, "Meta")
+    _REFERENCE_OP_LIB.append(lib)  # keep the registration alive
+    return True
+
+
+_REFERENCE_OP_LIB: list = []
+REFERENCE_OP_NAMES_REGISTERED = _register_reference_op_names()
 
 
 def e4m3_cast(x):

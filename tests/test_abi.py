@@ -67,10 +67,14 @@ def test_op_library_registers_schemas():
     assert "int num_bits, int exponent_bits, bool unsigned, bool narrow_range" in schema
 
 
-def test_cpu_tensor_fails_loudly():
-    """No CPU compute path in the product: a CPU tensor raises instead of falling back."""
+def test_cpu_tensor_fails_loudly_outside_the_cpu_ops():
+    """The reference's "cpu" registration covers quantize_op (INT / FP8, tensor_quant.py:252-256)
+    and the product has host kernels for it; ops without a CPU kernel raise on a CPU tensor
+    instead of falling back to anything."""
     with pytest.raises((RuntimeError, NotImplementedError)):
-        _ext.ops().quantize_op(torch.randn(4, 4), torch.tensor(1.0), 8, 0, False, True)
+        _ext.ops().fused_amax_convert(torch.randn(4, 32), 32, 6, 9, None)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        _ext.ops().histogram_abs_accumulate(torch.randn(64), torch.ones(1), torch.zeros(8, dtype=torch.int32), 8, False)
 
 
 def test_meta_kernels():

@@ -160,6 +160,7 @@ def test_fused_experts_conversion_matches_reference():
 
 
 def test_max_calibrator_skips_same_view():
+    from modelopt_amd.torch.quantization.calib import max as max_mod
     from modelopt_amd.torch.quantization.calib.max import MaxCalibrator
 
     p = nn.Parameter(torch.randn(4, 8, 16))
@@ -169,9 +170,12 @@ def test_max_calibrator_skips_same_view():
     base, key = c._view_key(p[2])
     import weakref
 
-    c._last = (weakref.ref(base), key, p[2]._version)
+    c._last = (weakref.ref(base), key, p[2]._version, max_mod._EPOCH)
     assert c._same_as_last(p[2])  # a fresh view of the same slice
     assert not c._same_as_last(p[1])
+    max_mod.new_collect_epoch()
+    assert not c._same_as_last(p[2])  # a new collection pass forgets the key
+    c._last = (weakref.ref(base), key, p[2]._version, max_mod._EPOCH)
     with torch.no_grad():
         p.mul_(2)
     assert not c._same_as_last(p[2])  # version bumped
