@@ -256,6 +256,22 @@ int mtq_awq_clip_search(const void *w, const float *x, int64_t co, int64_t cols,
                         int n_shrinks, int block, int num_bits, int is_unsigned, int narrow_range,
                         float *loss, int accumulate, hipStream_t stream);
 
+/* ---- AWQ-lite alpha search GEMM (MFMA) ---------------------------------------------------
+ * Replaces, for all G alphas of one linear and one calibration batch, the reference's search
+ * forward + update_loss (model_calib.py:1513-1560, :1489-1495):
+ *   loss[g] += mean_{m,n} float(T(T(sum_k T(x[m,k]*sinv[g,k]) * wq[g,n,k] + bias[n]) - yref[m,n]))^2
+ * x [M, K], sinv [G, K] (= (1/s_g).to(T)), wq [G, N, K] (= qdq(W * s_g), mtq_block_quant_dynamic),
+ * bias [N] or NULL, yref [M, N] (the unquantized output), all dtype T (bf16 / f16), 16-byte
+ * aligned, K % 64 == 0, N % 8 == 0, M*K and N*K < 2^31; fp32 accumulation on v_mfma_f32_32x32x16; the output is never stored.
+ * workspace: mtq_awq_search_gemm_workspace_floats(M, N, K, G) floats, 16-byte aligned, no
+ * initialisation needed (per-tile partial sums + the pre-scaled activations [G, M, K]).
+ * Deterministic (fixed-order sums).  G <= 64. */
+int64_t mtq_awq_search_gemm_workspace_floats(int64_t M, int64_t N, int64_t K, int G);
+int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const void *bias,
+                        const void *yref, int64_t M, int64_t N, int64_t K, int dtype, int G,
+                        float *loss, float *workspace, int64_t workspace_floats,
+                        hipStream_t stream);
+
 /* ---- host (CPU) kernels: the reference's "cpu" op registration ---------------------------
  * The reference registers tensorrt::quantize_op for ["cpu", "cuda"] (tensor_quant.py:252-256)
  * and runs `_tensor_quant` (:607-645), `_fp8_eager` (:46-59) and `reduce_amax`

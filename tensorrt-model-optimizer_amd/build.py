@@ -53,7 +53,8 @@ def _run(cmd: list[str]) -> None:
 
 def build_kernels(force: bool = False) -> Path:
     out = OUT / "libmtq_amd.so"
-    srcs = [CSRC / "mtq_kernels.hip", CSRC / "mtq_search.hip", CSRC / "mtq_qlinear.hip", CSRC / "mtq_cpu.cpp"]
+    srcs = [CSRC / "mtq_kernels.hip", CSRC / "mtq_search.hip", CSRC / "mtq_qlinear.hip", CSRC / "mtq_awq_gemm.hip",
+            CSRC / "mtq_cpu.cpp"]
     deps = srcs + [CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
     if force or _stale(out, deps):
         OUT.mkdir(parents=True, exist_ok=True)

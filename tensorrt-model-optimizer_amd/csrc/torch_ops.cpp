@@ -415,6 +415,43 @@ void mse_accumulate(const at::Tensor &a, const at::Tensor &b, at::Tensor loss, i
   check_status(st, "mse_accumulate");
 }
 
+// AWQ-lite alpha search, all alphas of one linear in one MFMA launch (mtq_awq_search_gemm):
+// loss[g] += mean((T(T(x * sinv[g]) @ wq[g]^T + bias) - yref)^2), the GEMM output never stored.
+void awq_search_gemm(const at::Tensor &x, const at::Tensor &sinv, const at::Tensor &wq,
+                     const c10::optional<at::Tensor> &bias, const at::Tensor &yref, at::Tensor loss) {
+  check_device(x, "x");
+  check_device(wq, "wq");
+  check_device(yref, "yref");
+  const int dt = checked_dtype(x, "x");
+  TORCH_CHECK(dt == MTQ_BF16 || dt == MTQ_F16, "awq_search_gemm: bf16 / f16 only");
+  TORCH_CHECK(sinv.scalar_type() == x.scalar_type() && wq.scalar_type() == x.scalar_type() &&
+                  yref.scalar_type() == x.scalar_type(),
+              "awq_search_gemm: x, sinv, wq and yref must share the dtype");
+  TORCH_CHECK(wq.dim() == 3 && sinv.dim() == 2, "awq_search_gemm: wq [G, N, K], sinv [G, K]");
+  const int64_t G = wq.size(0), N = wq.size(1), K = wq.size(2);
+  TORCH_CHECK(x.size(-1) == K && sinv.size(0) == G && sinv.size(1) == K,
+              "awq_search_gemm: shape mismatch");
+  at::Tensor xc = x.contiguous().view({-1, K});
+  const int64_t M = xc.size(0);
+  TORCH_CHECK(yref.numel() == M * N && yref.size(-1) == N, "awq_search_gemm: yref must be [..., N]");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.is_contiguous() && loss.numel() == G,
+              "awq_search_gemm: loss must be a contiguous fp32 tensor with G elements");
+  at::Tensor sc = sinv.contiguous(), wc = wq.contiguous(), yc = yref.contiguous();
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->contiguous();
+    TORCH_CHECK(b.scalar_type() == x.scalar_type() && b.numel() == N, "awq_search_gemm: bias");
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t wf = mtq_awq_search_gemm_workspace_floats(M, N, K, (int)G);
+  at::Tensor ws = at::empty({std::max<int64_t>(wf, 1)}, x.options().dtype(at::kFloat));
+  int st = mtq_awq_search_gemm(xc.data_ptr(), sc.data_ptr(), wc.data_ptr(),
+                               b.defined() ? b.data_ptr() : nullptr, yc.data_ptr(), M, N, K, dt,
+                               (int)G, loss.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(),
+                               cur_stream(xc));
+  check_status(st, "awq_search_gemm");
+}
+
 at::Tensor mul_cols(const at::Tensor &x, const at::Tensor &scale) {
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
@@ -643,6 +680,30 @@ at::Tensor block_quant_dynamic(const at::Tensor &inputs, const c10::optional<at:
   return y;
 }
 
+// The weight side of every AWQ alpha at once: out[g] = qdq_block(T(W * pqs[g])), out [G, N, K]
+// (G launches of mtq_block_quant_dynamic writing straight into the stacked output).
+at::Tensor block_quant_dynamic_multi(const at::Tensor &inputs, const at::Tensor &pqs, int64_t block,
+                                     int64_t num_bits, bool is_unsigned, bool narrow_range) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  const int dt = checked_dtype(x, "inputs");
+  const int64_t cols = x.size(-1), rows = x.numel() / cols;
+  at::Tensor s = pqs.to(x.device(), x.scalar_type()).contiguous();
+  TORCH_CHECK(s.dim() == 2 && s.size(1) == cols, "block_quant_dynamic_multi: pqs must be [G, cols]");
+  const int64_t G = s.size(0);
+  at::Tensor y = at::empty({G, rows, cols}, x.options());
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const size_t esz = x.element_size();
+  for (int64_t g = 0; g < G; ++g) {
+    int st = mtq_block_quant_dynamic(
+        x.data_ptr(), static_cast<char *>(y.data_ptr()) + g * rows * cols * esz, rows, cols, dt,
+        static_cast<const char *>(s.data_ptr()) + g * cols * esz, dt, (int)block, (int)num_bits,
+        is_unsigned, narrow_range, cur_stream(x));
+    check_status(st, "block_quant_dynamic_multi");
+  }
+  return y;
+}
+
 // QuantLinear simulated GEMM for short inputs: y = x . qdq(W)^T (+ bias), weight fake quant fused
 // into the MFMA operand loads (mtq_qlinear_small_m).  kind 0 = INT-n, 1 = FP8 e4m3.
 at::Tensor qlinear_small_m(const at::Tensor &input, const at::Tensor &weight,
@@ -781,6 +842,9 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "int num_bits, bool unsigned, bool narrow_range) -> Tensor");
   m.def("mse_accumulate(Tensor a, Tensor b, Tensor(a!) loss, int index) -> ()");
   m.def("mul_cols(Tensor inputs, Tensor scale) -> Tensor");
+  m.def("block_quant_dynamic_multi(Tensor inputs, Tensor pqs, int block, int num_bits, bool unsigned, "
+        "bool narrow_range) -> Tensor");
+  m.def("awq_search_gemm(Tensor x, Tensor sinv, Tensor wq, Tensor? bias, Tensor yref, Tensor(a!) loss) -> ()");
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
   m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
   m.def("fp4_block_scale_quant(Tensor inputs, Tensor scales) -> Tensor");
@@ -811,6 +875,8 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);
   m.impl("mse_accumulate", &mse_accumulate);
   m.impl("mul_cols", &mul_cols);
+  m.impl("awq_search_gemm", &awq_search_gemm);
+  m.impl("block_quant_dynamic_multi", &block_quant_dynamic_multi);
   m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);
   m.impl("fp4_block_scale_quant", &fp4_block_scale_quant);
   m.impl("export_fp8", &export_fp8);

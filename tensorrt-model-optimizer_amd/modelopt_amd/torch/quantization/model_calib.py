@@ -14,6 +14,7 @@
 from __future__ import annotations
 
 import math
+import os
 import warnings
 from collections.abc import Callable
 
@@ -341,6 +342,71 @@ def _mse_fast(out, ref) -> bool:
     )
 
 
+# Fused AWQ search on MFMA (csrc/mtq_awq_gemm.hip): used for linears with at most this many output
+# features, where it beats the per-alpha hipBLASLt path (k/v_proj: 1.4-1.6x, scripts/bench_awq_gemm.py);
+# wider linears keep hipBLASLt for the GEMM (its 1.5 PFLOP/s vs the fused kernel's ~1.0).
+# MTQ_AMD_AWQ_FUSED: "auto" (default), "always", "never".
+_AWQ_FUSED_MAX_N = 2048
+_AWQ_FUSED = os.environ.get("MTQ_AMD_AWQ_FUSED", "auto")
+# Budget for keeping every alpha's quantised weight [11, N, K] across the search batches (it does
+# not change between batches; the reference recomputes it per batch): a fraction of the HBM free
+# when the search pass starts (Llama-3-8B: 154 GB of 288 GB).
+_AWQ_WQ_CACHE_FRACTION = float(os.environ.get("MTQ_AMD_AWQ_WQ_CACHE_FRACTION", "0.6"))
+_awq_wq_budget = [0]
+
+
+def _awq_search_tables(helper, dtype):
+    """Per-alpha scales of the whole search, [G, K] each: pre_quant_scale of the weight side and
+    of the input side, exactly as the per-alpha code computes them (get_scale, then
+    ``(1 / s).to(dtype)`` / ``s.to(dtype)``), stacked once per linear."""
+    if getattr(helper, "_tables", None) is None:
+        s = torch.stack([get_scale(helper.act_scale, helper.weight_scale, a, None) for a in helper.alphas])
+        helper._tables = ((1 / s).to(dtype), s.to(dtype))
+    return helper._tables
+
+
+def _awq_wq_all(self, helper, pqs_w, blk):
+    wq = getattr(helper, "_wq_all", None)
+    if wq is not None:
+        return wq
+    q = self.weight_quantizer
+    wq = _ops().block_quant_dynamic_multi(self.weight.detach(), pqs_w, blk, q._num_bits, q._unsigned,
+                                          q._narrow_range)
+    nbytes = wq.numel() * wq.element_size()
+    if nbytes <= _awq_wq_budget[0]:
+        _awq_wq_budget[0] -= nbytes
+        helper._wq_all = wq
+    return wq
+
+
+def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
+    """All alphas of one search batch with the weight side computed once per linear; the GEMM +
+    loss either fused on MFMA (narrow linears) or per alpha on hipBLASLt.  False when the
+    module / tensors do not qualify (the generic per-alpha path then runs)."""
+    w = self.weight
+    if not (
+        isinstance(out_act, torch.Tensor) and out_act.is_cuda and out_act.dtype == w.dtype
+        and input.is_cuda and input.dtype == w.dtype and w.dtype in (torch.bfloat16, torch.float16)
+        and not self.output_quantizer.is_enabled and not self.input_quantizer.is_enabled
+        and input.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0
+        and out_act.shape[-1] == w.shape[0] and out_act.numel() // w.shape[0] == input.numel() // w.shape[1]
+    ):
+        return False
+    sinv, pqs_w = _awq_search_tables(helper, w.dtype)
+    wq = _awq_wq_all(self, helper, pqs_w, blk)
+    ops = _ops()
+    bias = self.bias.detach() if self.bias is not None else None
+    x2 = input.reshape(-1, input.shape[-1])
+    fused = _AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and w.shape[0] <= _AWQ_FUSED_MAX_N)
+    if fused:
+        ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
+    else:
+        for ai in range(len(helper.alphas)):
+            out = F.linear(ops.mul_cols(x2, sinv[ai]), wq[ai], bias)
+            ops.mse_accumulate(out, out_act.reshape(-1, w.shape[0]), helper.loss, ai)
+    return True
+
+
 def _awq_forward(self, input, *args, **kwargs):
     """Patched QuantLinear forward during AWQ-lite (reference :1513-1560)."""
     helper = self.awq_lite
@@ -366,6 +432,12 @@ def _awq_forward(self, input, *args, **kwargs):
 
     fast, blk = _weight_qdq_fast_path(self.weight_quantizer, self.weight)
     out_act = out_actual[0] if isinstance(out_actual, tuple) else out_actual
+    if (
+        fast and not args and not kwargs and type(self)._original_cls is nn.Linear
+        and _AWQ_FUSED != "never" and _awq_search_fast(self, helper, input, out_act, blk)
+    ):
+        helper.num_search_steps += 1
+        return out_actual
     ops = _ops()
     x_fast = (
         input.is_cuda and input.dtype == self.weight.dtype and input.dtype in _FAST_DTYPES
@@ -462,7 +534,16 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
             module.awq_lite.is_enabled = False
 
     _AWQLiteHelper.cache_mode = False
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+        _awq_wq_budget[0] = int(torch.cuda.mem_get_info()[0] * _AWQ_WQ_CACHE_FRACTION)
     forward_loop(model)
+    _awq_wq_budget[0] = 0
+    for _, module in model.named_modules():
+        h = getattr(module, "awq_lite", None)
+        if isinstance(h, _AWQLiteHelper):
+            h._wq_all = None
+            h._tables = None
 
     def postprocess(module, name):
         h = module.awq_lite

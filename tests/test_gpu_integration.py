@@ -82,9 +82,9 @@ def test_reference_op_names_on_device(gpu):
     y = torch.ops.tensorrt.quantize_op(x.to(gpu), a.to(gpu), 4, 0, False, False)
     assert _same(y.cpu(), R.tensor_quant(x, a, 4, False, False))
     # MXFP4 (E2M1, E8M0 scales): the None-amax overload
-    y = torch.ops.tensorrt.dynamic_block_quantize_op(x.to(gpu), 32, None, 4, 2, 8, 8)
+    y = torch.ops.tensorrt.dynamic_block_quantize_op(x.to(gpu), 32, None, 4, 2, 9, 8)
     assert _same(y.cpu(), R.fused_amax_convert(x, 32, "E2M1"))
-    y = torch.ops.tensorrt.dynamic_block_quantize_op.overload(x.to(gpu), 32, None, 4, 2, 8, 8)
+    y = torch.ops.tensorrt.dynamic_block_quantize_op.overload(x.to(gpu), 32, None, 4, 2, 9, 8)
     assert _same(y.cpu(), R.fused_amax_convert(x, 32, "E2M1"))
     # meta (torch.export / fake tensors)
     m = torch.ops.tensorrt.quantize_op(x.to("meta"), a.to("meta"), 8, 4, False, False)
