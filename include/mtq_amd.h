@@ -271,6 +271,17 @@ int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const v
                         const void *yref, int64_t M, int64_t N, int64_t K, int dtype, int G,
                         float *loss, float *workspace, int64_t workspace_floats,
                         hipStream_t stream);
+/* The same search with the GEMMs elsewhere (wide linears keep hipBLASLt):
+ *  mtq_awq_prescale: xs[g, m, k] = T(x[m, k] * sinv[g, k]), one read of x for all G alphas
+ *    (the reference's `inputs * pre_quant_scale` per alpha, tensor_quantizer.py:1143-1144).
+ *  mtq_awq_mse_multi: loss[g] += mean(float(T(out[g] - ref))^2) over n elements for all G <= 16
+ *    outputs [G, n] (update_loss, model_calib.py:1489-1495), reading ref once; workspace of
+ *    mtq_awq_mse_multi_workspace_floats(n, G) floats; deterministic. */
+int mtq_awq_prescale(const void *x, const void *sinv, void *xs, int64_t M, int64_t K, int dtype, int G,
+                     hipStream_t stream);
+int64_t mtq_awq_mse_multi_workspace_floats(int64_t n, int G);
+int mtq_awq_mse_multi(const void *out, const void *ref, int64_t n, int dtype, int G, float *loss,
+                      float *workspace, int64_t workspace_floats, hipStream_t stream);
 
 /* ---- host (CPU) kernels: the reference's "cpu" op registration ---------------------------
  * The reference registers tensorrt::quantize_op for ["cpu", "cuda"] (tensor_quant.py:252-256)

@@ -1,11 +1,13 @@
 #!/bin/bash
-# AWQ tests, then C3 (Llama-3-8B INT4_AWQ_CFG, 512 x 512) wall-clock and a 128-sample kernel trace.
+# Wide AWQ path probe (each step synchronised), then AWQ tests, C3 512 x 512, 128-sample trace.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 R="$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_awq_gemm.py tests/test_gpu_mtq.py tests/test_gpu_dp.py -m gpu -q -x -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/awq_tests.log 2>&1 || { tail -30 gpurun_out/awq_tests.log; exit 10; }
+timeout -k 10 200 python -u scripts/debug/awq_wide_probe.py > gpurun_out/wide_probe.log 2>&1 || { tail -20 gpurun_out/wide_probe.log; exit 9; }
+cat gpurun_out/wide_probe.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_awq_gemm.py tests/test_gpu_mtq.py -m gpu -q -x -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/awq_tests.log 2>&1 || { tail -30 gpurun_out/awq_tests.log; exit 10; }
 tail -1 gpurun_out/awq_tests.log
 timeout -k 10 400 python -u scripts/ptq_llama.py --config INT4_AWQ_CFG --no-baseline > gpurun_out/c3_512.json 2> gpurun_out/c3_512.err || { tail -20 gpurun_out/c3_512.err; exit 11; }
 tail -1 gpurun_out/c3_512.json

@@ -340,6 +340,43 @@ __global__ __launch_bounds__(256) void awq_prescale_kernel(const T *__restrict__
   }
 }
 
+// The loss of all G alphas from materialised outputs (the wide linears, whose GEMMs stay on
+// hipBLASLt): reads the reference output once and each alpha's output once,
+// partial[g * grid + block] = sum over the block's elements of float(T(out[g] - ref))^2.
+template <typename T>
+__global__ __launch_bounds__(256) void awq_mse_multi_kernel(const T *__restrict__ out, const T *__restrict__ ref,
+                                                            int64_t chunks, int G, float *__restrict__ partial) {
+  __shared__ float red[16][256];
+  float acc[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < chunks; c += (int64_t)gridDim.x * 256) {
+    const Vec<T> r = ldg_vec_nt(ref + c * 8);
+    float rf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rf[j] = Elem<T>::ld(r.e[j]);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if (g >= G) break;
+      const Vec<T> o = ldg_vec_nt(out + ((int64_t)g * chunks + c) * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = Elem<T>::ld(Elem<T>::st(Elem<T>::ld(o.e[j]) - rf[j]));
+        acc[g] = __builtin_fmaf(d, d, acc[g]);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 16; ++g) red[g][threadIdx.x] = acc[g];
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int g = 0; g < G; ++g) red[g][threadIdx.x] += red[g][threadIdx.x + o];
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < G) partial[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = red[threadIdx.x][0];
+}
+
 // loss[g] += (sum over the group's tiles, in double, fixed order) / (M * N)
 __global__ __launch_bounds__(256) void awq_search_finish_kernel(const float *partial, int tiles, int G,
                                                                  double inv_count, float *loss) {
@@ -451,5 +488,48 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
   if (st != MTQ_OK) return st;
   awq_search_finish_kernel<<<1, 256, 0, stream>>>(workspace, (int)tiles, G, 1.0 / ((double)M * (double)N),
                                                   loss);
+  return host_check_launch();
+}
+
+extern "C" int64_t mtq_awq_mse_multi_workspace_floats(int64_t n, int G) {
+  if (n < 1 || G < 1) return 0;
+  const int64_t chunks = n / 8;
+  int64_t grid = (chunks + 255) / 256;
+  grid = grid < 2048 ? grid : 2048;
+  return grid * G;
+}
+
+extern "C" int mtq_awq_mse_multi(const void *out, const void *ref, int64_t n, int dtype, int G, float *loss,
+                                 float *workspace, int64_t workspace_floats, hipStream_t stream) {
+  if (n < 8 || n % 8 != 0 || G < 1 || G > 16 || !out || !ref || !loss || !workspace) return MTQ_ERR_INVALID_ARG;
+  if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
+  if (!al16(out) || !al16(ref)) return MTQ_ERR_INVALID_ARG;
+  const int64_t grid = mtq_awq_mse_multi_workspace_floats(n, G) / G;
+  if (workspace_floats < grid * G) return MTQ_ERR_INVALID_ARG;
+  if (dtype == MTQ_BF16)
+    awq_mse_multi_kernel<__bf16><<<(unsigned)grid, 256, 0, stream>>>((const __bf16 *)out, (const __bf16 *)ref,
+                                                                    n / 8, G, workspace);
+  else
+    awq_mse_multi_kernel<_Float16><<<(unsigned)grid, 256, 0, stream>>>((const _Float16 *)out,
+                                                                      (const _Float16 *)ref, n / 8, G, workspace);
+  int st = host_check_launch();
+  if (st != MTQ_OK) return st;
+  awq_search_finish_kernel<<<1, 256, 0, stream>>>(workspace, (int)grid, G, 1.0 / (double)n, loss);
+  return host_check_launch();
+}
+
+extern "C" int mtq_awq_prescale(const void *x, const void *sinv, void *xs, int64_t M, int64_t K, int dtype, int G,
+                                hipStream_t stream) {
+  if (M < 1 || K < 8 || K % 8 != 0 || G < 1 || !x || !sinv || !xs) return MTQ_ERR_INVALID_ARG;
+  if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
+  if (!al16(x) || !al16(sinv) || !al16(xs)) return MTQ_ERR_INVALID_ARG;
+  const int64_t chunks = M * K / 8;
+  const unsigned gb = (unsigned)((chunks + 255) / 256);
+  if (dtype == MTQ_BF16)
+    awq_prescale_kernel<__bf16><<<gb, 256, 0, stream>>>((const __bf16 *)x, (const __bf16 *)sinv, (__bf16 *)xs,
+                                                        chunks, K / 8, G);
+  else
+    awq_prescale_kernel<_Float16><<<gb, 256, 0, stream>>>((const _Float16 *)x, (const _Float16 *)sinv,
+                                                          (_Float16 *)xs, chunks, K / 8, G);
   return host_check_launch();
 }

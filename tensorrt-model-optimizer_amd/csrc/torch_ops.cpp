@@ -452,6 +452,42 @@ void awq_search_gemm(const at::Tensor &x, const at::Tensor &sinv, const at::Tens
   check_status(st, "awq_search_gemm");
 }
 
+// xs [G, M, K] = T(x * sinv[g]) for every alpha (mtq_awq_prescale)
+at::Tensor awq_prescale(const at::Tensor &x, const at::Tensor &sinv) {
+  check_device(x, "x");
+  const int dt = checked_dtype(x, "x");
+  TORCH_CHECK(dt == MTQ_BF16 || dt == MTQ_F16, "awq_prescale: bf16 / f16 only");
+  const int64_t K = x.size(-1);
+  at::Tensor xc = x.contiguous().view({-1, K});
+  at::Tensor sc = sinv.to(x.device(), x.scalar_type()).contiguous();
+  TORCH_CHECK(sc.dim() == 2 && sc.size(1) == K, "awq_prescale: sinv must be [G, K]");
+  at::Tensor y = at::empty({sc.size(0), xc.size(0), K}, x.options());
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_awq_prescale(xc.data_ptr(), sc.data_ptr(), y.data_ptr(), xc.size(0), K, dt,
+                                (int)sc.size(0), cur_stream(xc)),
+               "awq_prescale");
+  return y;
+}
+
+// loss[g] += mean((out[g] - ref)^2) for all g at once (mtq_awq_mse_multi)
+void awq_mse_multi(const at::Tensor &out, const at::Tensor &ref, at::Tensor loss) {
+  check_device(out, "out");
+  check_device(ref, "ref");
+  const int dt = checked_dtype(out, "out");
+  TORCH_CHECK(ref.scalar_type() == out.scalar_type(), "awq_mse_multi: dtype mismatch");
+  const int64_t G = out.size(0), n = ref.numel();
+  TORCH_CHECK(out.numel() == G * n, "awq_mse_multi: out must be [G, *ref.shape]");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.is_contiguous() && loss.numel() == G,
+              "awq_mse_multi: loss must be a contiguous fp32 tensor with G elements");
+  at::Tensor oc = out.contiguous(), rc = ref.contiguous();
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(out.device());
+  const int64_t wf = mtq_awq_mse_multi_workspace_floats(n, (int)G);
+  at::Tensor ws = at::empty({std::max<int64_t>(wf, 1)}, out.options().dtype(at::kFloat));
+  check_status(mtq_awq_mse_multi(oc.data_ptr(), rc.data_ptr(), n, dt, (int)G, loss.data_ptr<float>(),
+                                 ws.data_ptr<float>(), ws.numel(), cur_stream(oc)),
+               "awq_mse_multi");
+}
+
 at::Tensor mul_cols(const at::Tensor &x, const at::Tensor &scale) {
   check_device(x, "inputs");
   const int dt = checked_dtype(x, "inputs");
@@ -844,6 +880,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("mul_cols(Tensor inputs, Tensor scale) -> Tensor");
   m.def("block_quant_dynamic_multi(Tensor inputs, Tensor pqs, int block, int num_bits, bool unsigned, "
         "bool narrow_range) -> Tensor");
+  m.def("awq_prescale(Tensor x, Tensor sinv) -> Tensor");
+  m.def("awq_mse_multi(Tensor out, Tensor ref, Tensor(a!) loss) -> ()");
   m.def("awq_search_gemm(Tensor x, Tensor sinv, Tensor wq, Tensor? bias, Tensor yref, Tensor(a!) loss) -> ()");
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
   m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
@@ -876,6 +914,8 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("mse_accumulate", &mse_accumulate);
   m.impl("mul_cols", &mul_cols);
   m.impl("awq_search_gemm", &awq_search_gemm);
+  m.impl("awq_prescale", &awq_prescale);
+  m.impl("awq_mse_multi", &awq_mse_multi);
   m.impl("block_quant_dynamic_multi", &block_quant_dynamic_multi);
   m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);
   m.impl("fp4_block_scale_quant", &fp4_block_scale_quant);

@@ -400,6 +400,22 @@ def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
     fused = _AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and w.shape[0] <= _AWQ_FUSED_MAX_N)
     if fused:
         ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
+    elif len(helper.alphas) <= 16:
+        # wide linears: x * (1/s) for every alpha in one pass, the alphas' GEMMs as one batched
+        # hipBLASLt call (bias in its fp32 epilogue, one rounding, as F.linear), all losses in
+        # one pass that reads out_actual once
+        # (per-alpha torch.mm into slices of one [G, M, N] output, the GEMM F.linear itself uses:
+        # torch.bmm with the transposed [G, K, N] weight view faulted the GPU in hipBLASLt on
+        # ROCm 7 at [11, 8192, 4096] x [11, 4096, 4096])
+        xs = ops.awq_prescale(x2, sinv)
+        out = torch.empty((xs.shape[0], xs.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+        for ai in range(xs.shape[0]):
+            if bias is None:
+                torch.mm(xs[ai], wq[ai].t(), out=out[ai])
+            else:
+                torch.addmm(bias, xs[ai], wq[ai].t(), out=out[ai])
+        del xs
+        ops.awq_mse_multi(out, out_act.reshape(-1, w.shape[0]), helper.loss)
     else:
         for ai in range(len(helper.alphas)):
             out = F.linear(ops.mul_cols(x2, sinv[ai]), wq[ai], bias)

@@ -135,11 +135,13 @@ def _awq_run(gpu, mode):
     return m
 
 
-def test_awq_lite_fused_search_matches_per_alpha_path(gpu):
-    """awq_lite end to end with the fused MFMA search ("always") vs the per-alpha hipBLASLt path
-    ("never"): per-alpha losses within rtol 2e-3 (GEMM summation order), the same best alpha, and
-    then the same scales, weights and amax bit for bit."""
-    fused, ref = _awq_run(gpu, "always"), _awq_run(gpu, "never")
+@pytest.mark.parametrize("mode", ["always", "auto"])
+def test_awq_lite_fused_search_matches_per_alpha_path(gpu, mode):
+    """awq_lite end to end with the fused MFMA search ("always"; "auto" sends the 2048-wide
+    linear and narrower ones to it and the rest to batched hipBLASLt + the multi-alpha loss pass)
+    vs the per-alpha hipBLASLt path ("never"): per-alpha losses within rtol 2e-3 (GEMM summation
+    order), the same best alpha, and then the same scales, weights and amax bit for bit."""
+    fused, ref = _awq_run(gpu, mode), _awq_run(gpu, "never")
     for name in ("up", "mid", "down"):
         hf, hr = getattr(fused, name).awq_lite, getattr(ref, name).awq_lite
         torch.testing.assert_close(hf.loss, hr.loss, rtol=2e-3, atol=0)
@@ -147,3 +149,22 @@ def test_awq_lite_fused_search_matches_per_alpha_path(gpu):
         assert torch.equal(hf.best_scale, hr.best_scale)
         assert torch.equal(getattr(fused, name).weight, getattr(ref, name).weight)
         assert torch.equal(getattr(fused, name).weight_quantizer.amax, getattr(ref, name).weight_quantizer.amax)
+
+
+@pytest.mark.parametrize("G", [1, 11, 16])
+def test_prescale_and_mse_multi(gpu, G):
+    gen = torch.Generator(device=gpu).manual_seed(G)
+    x = torch.randn(300, 512, device=gpu, generator=gen).to(torch.bfloat16)
+    s = (torch.rand(G, 512, device=gpu, generator=gen) + 0.5).to(torch.bfloat16)
+    xs = _ext.ops().awq_prescale(x, s)
+    for g in range(G):
+        assert torch.equal(xs[g], x * s[g])  # the reference's bf16 multiply, bit for bit
+    ref = torch.randn(300, 256, device=gpu, generator=gen).to(torch.bfloat16)
+    out = torch.randn(G, 300, 256, device=gpu, generator=gen).to(torch.bfloat16)
+    loss = torch.zeros(G, device=gpu)
+    _ext.ops().awq_mse_multi(out, ref, loss)
+    want = torch.stack([(out[g] - ref).float().pow(2).mean() for g in range(G)])
+    torch.testing.assert_close(loss, want, rtol=1e-5, atol=0)
+    again = torch.zeros(G, device=gpu)
+    _ext.ops().awq_mse_multi(out, ref, again)
+    assert torch.equal(loss, again)
