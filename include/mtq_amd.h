@@ -203,6 +203,11 @@ int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int 
                      hipStream_t stream);
 int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int dtype, int block,
                      hipStream_t stream);
+/* MXFP8QTensor.quantize (qtensor/mxfp8_tensor.py:163-187; the MXFP8 branch of the unified export,
+ * export/unified_export_hf.py:671-680 + quant_utils.py:309-310, 871-872): x bf16/f16 with
+ * n % 32 == 0, blocks of 32 consecutive elements; y n e4m3 bytes, scales n/32 E8M0 bytes. */
+int mtq_export_mxfp8(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int dtype,
+                     hipStream_t stream);
 
 /* ---- AWQ-lite search helpers ---------------------------------------------------------------
  * loss[0] += mean(float(T(a - b))^2) over n elements of dtype T: the per-alpha search loss

@@ -689,3 +689,23 @@ def awq_clip_best(losses, w_amax, shrinks):
         best_loss = torch.where(idx, loss, best_loss)
         best = torch.where(idx, w_amax * shrink, best)
     return best
+
+
+# ----------------------------------------------------------------------------------------------
+# MXFP8 (E4M3 elements, E8M0 scale per 32): restates MXFP8QTensor._compute_e8m0_exponent +
+# quantize_with_scale, quantization/qtensor/mxfp8_tensor.py:36-52, 140-187
+# ----------------------------------------------------------------------------------------------
+
+
+def mxfp8_quantize(weight, block=32):
+    """(e4m3 codes as float8_e4m3fn, E8M0 bytes [..., K/32]) of a [..., K] weight, K % 32 == 0."""
+    shape = weight.shape
+    blocks = weight.reshape(*shape[:-1], shape[-1] // block, block)
+    amax = blocks.abs().amax(dim=-1)
+    descale = amax.float() / 448.0
+    log2 = torch.where(descale > 0, torch.log2(descale), torch.tensor(-127.0))
+    e = torch.clamp(torch.ceil(log2), min=-127, max=127)
+    s = (e + 127).to(torch.uint8)
+    f = torch.exp2(127 - s.float()).unsqueeze(-1)
+    q = (blocks * f).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).reshape(shape)
+    return q, s

@@ -2150,6 +2150,53 @@ template <class F> void with_export_u(F &&f) {
 }
 unsigned export_grid(int64_t nvec, int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); }
 
+// MXFP8QTensor.quantize (qtensor/mxfp8_tensor.py:36-52 + 163-187): per 32-block along the rows,
+// amax = max|x| (NaN propagates), descale = amax / 448 (IEEE), e = clamp(ceil(log2(descale)),
+// -127, 127) with log2 correctly rounded and e = -127 where descale is not > 0 (0 or NaN, the
+// reference's torch.where); q = e4m3(clamp(x * 2^-e, -448, 448)) (RNE, NaN kept); scale byte
+// e + 127.  Four lanes per block, one 16-byte vector each; 8 e4m3 bytes per lane out.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_mxfp8_kernel(const T *__restrict__ x,
+                                                                 uint8_t *__restrict__ y,
+                                                                 uint8_t *__restrict__ sc,
+                                                                 int64_t nvec) {
+  const int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool ok = v < nvec;
+  Vec<T> xv;
+  if (ok)
+    xv = ldg_vec_nt(x + v * 8);
+  else
+    xv.raw = make_uint4(0, 0, 0, 0);
+  float f[8];
+  uint32_t m = 0;  // max of |x| bit patterns: NaN patterns sort above +inf
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f[j] = Elem<T>::ld(xv.e[j]);
+    const uint32_t b = __float_as_uint(f[j]) & 0x7fffffffu;
+    m = b > m ? b : m;
+  }
+  m = max(m, (uint32_t)__shfl_xor((int)m, 1));
+  m = max(m, (uint32_t)__shfl_xor((int)m, 2));
+  const float amax = __uint_as_float(m > 0x7f800000u ? 0x7fc00000u : m);
+  const float descale = amax / 448.0f;
+  float e = descale > 0.f ? mx_e8m0_exponent(descale) : -127.f;
+  e = e < 127.f ? e : 127.f;
+  const float p = __builtin_ldexpf(1.0f, -(int)e);
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // torch's cast: NaN -> 0x7F | sign
+      packed |= e4m3_byte(clamp_nan(f[4 * h + j] * p, -kE4M3Max, kE4M3Max)) << (8 * j);
+    w[h] = packed;
+  }
+  if (ok) {
+    *reinterpret_cast<uint2 *>(y + v * 8) = make_uint2(w[0], w[1]);
+    if ((threadIdx.x & 3) == 0) sc[v >> 2] = (uint8_t)(int)(e + 127.f);
+  }
+}
+
 }  // namespace
 
 // shared with the other translation units of libmtq_amd.so (mtq_search.hip)
@@ -2584,6 +2631,21 @@ int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int 
       export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
           reinterpret_cast<const T *>(x), y, npairs, cols, block_scale, scale_2, block);
     }
+    return check_launch();
+  });
+}
+
+int mtq_export_mxfp8(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int dtype,
+                     hipStream_t stream) {
+  if (n < 0 || n % 32) return MTQ_ERR_INVALID_ARG;
+  if (n == 0) return MTQ_OK;
+  if (!x || !y || !scales || !aligned16(x) || ((uintptr_t)y & 7u)) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    if (Vec<T>::N != 8) return MTQ_ERR_DTYPE;  // 16-bit element types
+    const int64_t nvec = n / 8;
+    export_mxfp8_kernel<T><<<grid_for(nvec, kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), y, scales, nvec);
     return check_launch();
   });
 }

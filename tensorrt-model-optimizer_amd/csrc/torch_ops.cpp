@@ -613,6 +613,24 @@ std::tuple<at::Tensor, at::Tensor> export_mxfp4(const at::Tensor &weight, int64_
   return {y, sc};
 }
 
+// MXFP8: (e4m3 codes as float8_e4m3fn, same shape; E8M0 scale bytes [..., K/32])
+std::tuple<at::Tensor, at::Tensor> export_mxfp8(const at::Tensor &weight) {
+  check_device(weight, "weight");
+  const int dt = checked_dtype(weight, "weight");
+  TORCH_CHECK(dt == MTQ_BF16 || dt == MTQ_F16, "export_mxfp8: bf16 / f16 weights only");
+  TORCH_CHECK(weight.dim() >= 1 && weight.size(-1) % 32 == 0, "export_mxfp8: last dim % 32 != 0");
+  at::Tensor x = weight.contiguous();
+  at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
+  std::vector<int64_t> sshape(x.sizes().begin(), x.sizes().end());
+  sshape.back() = sshape.back() / 32;
+  at::Tensor sc = at::empty(sshape, x.options().dtype(at::kByte));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_export_mxfp8(x.data_ptr(), reinterpret_cast<uint8_t *>(y.data_ptr()),
+                                sc.data_ptr<uint8_t>(), x.numel(), dt, cur_stream(x)),
+               "export_mxfp8");
+  return {y, sc};
+}
+
 // ---- calibration searches (mtq_search.hip) ------------------------------------------------
 // nvfp4_fp8_scale_sweep(x [n_blocks, block], global_amax, candidates [126] fp32) -> best amax
 // [n_blocks] fp32 (kernels/quantization/gemm/nvfp4_fp8_sweep.py:108-160).
@@ -890,6 +908,7 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("export_int4(Tensor weight, Tensor scale) -> Tensor");
   m.def("export_nvfp4(Tensor weight, Tensor block_scale, Tensor scale_2) -> Tensor");
   m.def("export_mxfp4(Tensor weight, int block) -> (Tensor, Tensor)");
+  m.def("export_mxfp8(Tensor weight) -> (Tensor, Tensor)");
   m.def("nvfp4_fp8_scale_sweep(Tensor x, Tensor global_amax, Tensor candidates, int block_size=16) -> Tensor");
   m.def("mse_sweep(Tensor x, Tensor amax, Tensor candidates, int num_bits, bool unsigned, "
         "bool narrow_range, bool round_candidate_amax) -> Tensor");
@@ -923,6 +942,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("export_int4", &export_int4);
   m.impl("export_nvfp4", &export_nvfp4);
   m.impl("export_mxfp4", &export_mxfp4);
+  m.impl("export_mxfp8", &export_mxfp8);
   m.impl("nvfp4_fp8_scale_sweep", &nvfp4_fp8_scale_sweep);
   m.impl("mse_sweep", &mse_sweep);
   m.impl("awq_clip_search", &awq_clip_search);

@@ -327,6 +327,15 @@ def to_quantized_weight(weight, weights_scaling_factor, quantization, weights_sc
         return ops.export_nvfp4(weight, weights_scaling_factor.to(torch.float32), s2)
     if quantization in (QUANTIZATION_W4A8_MXFP4_FP8, QUANTIZATION_MXFP4):
         return mxfp4_quantize(weight, block_size)[0]
+    if quantization == QUANTIZATION_MXFP8:
+        # MXFP8QTensor.quantize_with_scale (reference :871-872): the HIP packer recomputes the
+        # same E8M0 scale from the weight; a scale from elsewhere takes the tensor expression
+        from ..quantization.qtensor import MXFP8QTensor
+
+        q, s = ops.export_mxfp8(weight)
+        if weights_scaling_factor is not None and not torch.equal(s, weights_scaling_factor.reshape(s.shape)):
+            q = MXFP8QTensor.quantize_with_scale(weight, weights_scaling_factor)
+        return q
     raise NotImplementedError(f"quantization format {quantization} not supported")
 
 

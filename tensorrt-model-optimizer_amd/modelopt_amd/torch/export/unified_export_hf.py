@@ -181,8 +181,16 @@ def _export_quantized_weight(sub_module: nn.Module, dtype: torch.dtype, weight_n
             oq._amax = oq._amax.to(torch.float32)
     else:
         if fmt == QUANTIZATION_MXFP8:
-            raise NotImplementedError("modelopt_amd: MXFP8 export is not implemented")
-        sub_module.register_buffer(names.weight_scale, get_weight_scaling_factor(sub_module, weight_name))
+            # E8M0 bytes per 32 (reference unified_export_hf.py:671-680)
+            from ..quantization.qtensor import MXFP8QTensor
+
+            sub_module.register_buffer(
+                names.weight_scale, MXFP8QTensor.get_weights_scaling_factor_from_quantizer(weight, wq)
+            )
+            if getattr(wq, "_scale", None) is not None:
+                del wq._scale
+        else:
+            sub_module.register_buffer(names.weight_scale, get_weight_scaling_factor(sub_module, weight_name))
         if iq is not None and iq.is_enabled and iq.amax is not None:
             sub_module.register_buffer(names.input_scale, get_activation_scaling_factor(sub_module, names.input_quantizer).squeeze())
 
@@ -272,6 +280,16 @@ def _process_quantized_modules(model: nn.Module, dtype: torch.dtype):
                 _export_quantized_weight(m, dtype)
             except AssertionError as e:
                 raise AssertionError(f"Failed to export module '{name}' (type={type(m).__name__}): {e}") from e
+        elif isinstance(m, nn.Embedding) and hasattr(m, "weight_quantizer"):
+            # a quantized embedding table, unless its weight is tied (reference
+            # hf_export_handlers.py:154-182)
+            if get_quantization_format(m) == QUANTIZATION_NONE:
+                continue
+            tied = [n for n, o in model.named_modules() if o is not m and getattr(o, "weight", None) is m.weight]
+            if tied:
+                warnings.warn(f"Skipping quantized weight packing for embedding '{name}': its weight is shared with {tied}.")
+                continue
+            _export_quantized_weight(m, dtype)
 
 
 def _export_dtype(model, dtype):

@@ -36,10 +36,30 @@ def modelopt_state(model: nn.Module) -> dict[str, Any]:
     if entry is None:
         return {"modelopt_state_dict": [], "modelopt_version": MODELOPT_VERSION}
     config = entry["config"]
-    return {
-        "modelopt_state_dict": [("quantize", {"config": config, "metadata": {"quantizer_state": quantizer_state(model)}})],
-        "modelopt_version": MODELOPT_VERSION,
-    }
+    modes = [("quantize", {"config": config, "metadata": {"quantizer_state": quantizer_state(model)}})]
+    if "compress" in entry:  # mtq.compress (reference compress.py:179-193)
+        modes.append(("real_quantize", {"config": entry["compress"]["config"],
+                                        "metadata": _compress_metadata(model)}))
+    return {"modelopt_state_dict": modes, "modelopt_version": MODELOPT_VERSION}
+
+
+def _compress_metadata(model: nn.Module) -> dict[str, Any]:
+    from ..quantization.compress import RealQuantLinear
+    from ..quantization.qtensor import QTensorWrapper
+
+    meta: dict[str, Any] = {"real_quantizer_state": {}, "q_tensor_state": {}}
+    for name, m in model.named_modules():
+        # RealQuantLinear modules, and any other module whose weight was packed (an nn.Embedding
+        # whose weight quantizer a config enabled is compressed by the reference too)
+        packed = isinstance(m._parameters.get("weight"), QTensorWrapper)
+        if isinstance(m, RealQuantLinear) or (packed and hasattr(m, "weight_quantizer")):
+            meta["real_quantizer_state"][name] = m.weight_quantizer.get_modelopt_state()
+            if packed:
+                st = m.weight.get_state()
+                md = dict(st["metadata"])
+                md["qtensor_class"] = md["qtensor_class"].__name__  # a name, not a class object
+                meta["q_tensor_state"][name] = {**st, "metadata": md}
+    return meta
 
 
 def _validate(state: Any) -> None:
@@ -70,6 +90,9 @@ def restore_from_modelopt_state(
             modelopt_state = torch.load(modelopt_state_path, map_location="cpu", weights_only=True)
     _validate(modelopt_state)
     for mode, entry in modelopt_state["modelopt_state_dict"]:
+        if mode == "real_quantize":
+            _restore_compressed(model, entry)
+            continue
         if mode != "quantize":
             continue  # calibration modes carry no architecture change
         config = QuantizeConfig(**entry["config"])
@@ -79,6 +102,31 @@ def restore_from_modelopt_state(
         restore_quantizer_state(model, config, entry["metadata"])
         model.__dict__["_modelopt_amd_mode"] = {"config": entry["config"]}
     return model
+
+
+def _restore_compressed(model: nn.Module, entry: dict) -> None:
+    """Re-create the packed weights' containers (shape / dtype / QTensor class) and the weight
+    quantizers' scale buffers so ``load_state_dict`` fills them (reference compress.py:136-176)."""
+    from ..quantization import qtensor as qt
+    from ..quantization.compress import CompressConfig, compress_convert
+    from ..quantization.qtensor import QTensorWrapper
+
+    cfg = CompressConfig(entry["config"].get("compress"), entry["config"].get("quant_gemm", True))
+    compress_convert(model, cfg, skip_real_quantize_weight=True)
+    meta = entry["metadata"]
+    for name, m in model.named_modules():
+        if name in meta.get("real_quantizer_state", {}):
+            m.weight_quantizer.set_from_modelopt_state(meta["real_quantizer_state"][name])
+            m.weight_quantizer._dequantize = True
+        if name in meta.get("q_tensor_state", {}):
+            st = meta["q_tensor_state"][name]
+            md = dict(st["metadata"])
+            md["qtensor_class"] = getattr(qt, md["qtensor_class"])
+            dev = m.weight.device
+            m._parameters["weight"] = QTensorWrapper(
+                torch.empty(st["quantized_data.shape"], dtype=st["quantized_data.dtype"], device=dev), metadata=md
+            )
+    model.__dict__.setdefault("_modelopt_amd_mode", {"config": {}})["compress"] = {"config": dict(cfg), "metadata": {}}
 
 
 def save(model: nn.Module, f: str | os.PathLike | BinaryIO, **kwargs) -> None:

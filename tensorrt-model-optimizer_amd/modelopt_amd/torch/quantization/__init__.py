@@ -27,3 +27,5 @@ from .nn.modules.tensor_quantizer import (
     register_quant_backend,
     unregister_quant_backend,
 )
+from . import qtensor
+from .compress import CompressConfig, RealQuantLinear, compress, is_real_quantized

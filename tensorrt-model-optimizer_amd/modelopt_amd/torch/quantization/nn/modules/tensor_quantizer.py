@@ -38,6 +38,7 @@ from ...tensor_quant import (
     fp8_fake_quant,
     quantize_op,
 )
+from ...qtensor.base_qtensor import BaseQuantizedTensor, QTensorWrapper
 from ...utils import core_utils as quant_utils
 
 __all__ = [
@@ -580,10 +581,72 @@ class TensorQuantizer(nn.Module):
             )
         return quantize_op(inputs, amax, self._num_bits, 0, self._unsigned, self._narrow_range)
 
-    def _real_quantize(self, inputs):
-        raise NotImplementedError(
-            "modelopt_amd: real quantization (compress / qtensor) is outside the fake-quant hot path"
+    # ---- real quantization (mtq.compress; reference :292-302, :788-888) ---------------------
+    def dequantize(self, inputs):
+        """Dequantise a packed weight (QTensorWrapper / QTensor) with the stored scales."""
+        qtensor = inputs.get_qtensor() if isinstance(inputs, QTensorWrapper) else inputs
+        assert isinstance(qtensor, BaseQuantizedTensor), "Expected input as real quantized tensors."
+        return qtensor.dequantize(
+            scale=getattr(self, "_scale", None),
+            block_sizes=self.block_sizes,
+            double_scale=getattr(self, "_double_scale", None),
+            scale_zeros=getattr(self, "_scale_zeros", None),
         )
+
+    def _set_buffer(self, key, value):
+        if hasattr(self, key) and key in self._buffers:
+            delattr(self, key)
+        self.register_buffer(key, value)
+
+    def _is_real_quantize_support(self):
+        return (
+            (self._num_bits == 4 and self._block_sizes)
+            or (self._num_bits == (2, 1) and self._block_sizes)
+            or self._num_bits in ((4, 3), 8)
+        )
+
+    def _real_quantize(self, inputs):
+        """Pack ``inputs`` into a QTensor and keep its scales as buffers (reference :796-888);
+        later forwards of the packed weight only dequantise."""
+        from ...qtensor import FP8QTensor, INT4QTensor, INT8QTensor, MXFP4QTensor, MXFP8QTensor, NVFP4QTensor
+        from ...qtensor.base_qtensor import true_div
+
+        assert self._is_real_quantize_support(), "Real quantization not supported for this format."
+        bs = self._block_sizes or {}
+        buffers = {}
+        if bs and bs.get("scale_bits") == (8, 0) and bs.get("type") == "dynamic":
+            if self._num_bits == (2, 1):
+                outputs, buffers["_scale"] = MXFP4QTensor.quantize(inputs, bs[-1])
+            elif self._num_bits == (4, 3):
+                assert bs[-1] == MXFP8QTensor.BLOCK_SIZE, (
+                    f"MXFP8 requires block size {MXFP8QTensor.BLOCK_SIZE}, got {bs[-1]}"
+                )
+                outputs, buffers["_scale"] = MXFP8QTensor.quantize(inputs)
+            else:
+                raise ValueError(f"Unsupported MX format: num_bits={self._num_bits}.")
+        elif self._num_bits == (4, 3):
+            use_amax = self.amax is not None and not (bs and self.amax.numel() == 1)
+            outputs, buffers["_scale"] = FP8QTensor.quantize(
+                inputs, axis=self._axis, block_sizes=bs or None,
+                scales=true_div(self.amax, 448.0) if use_amax else None,
+            )
+        elif self._num_bits == 8:
+            outputs, buffers["_scale"] = INT8QTensor.quantize(inputs, axis=self._axis, block_sizes=bs or None)
+        elif bs.get("scale_bits", 0) == 8 and bs.get("scale_block_sizes", None):
+            raise NotImplementedError("modelopt_amd: NF4 double quantization is not implemented")
+        elif bs.get("scale_bits") == (4, 3):
+            if bs.get("four_over_six", False):
+                raise NotImplementedError("NVFP4 Four-Over-Six (4/6) is not supported via mtq.compress.")
+            s2 = NVFP4QTensor.get_weights_scaling_factor_2_from_quantizer(self) if self.amax is not None else None
+            outputs, buffers["_scale"], buffers["_double_scale"] = NVFP4QTensor.quantize(
+                inputs, bs[-1], weights_scaling_factor_2=s2, try_tensorrt=True
+            )
+        else:
+            outputs, buffers["_scale"] = INT4QTensor.quantize(inputs, bs[-1])
+        for k, v in buffers.items():
+            self._set_buffer(k, v)
+        self._dequantize = True
+        return outputs
 
     # ---- static block quant reshapes (reference :975-1085) ------------------------------------
     # Semantics (pinned by the padding goldens, tests/test_gpu_golden.py): every blocked axis is
@@ -686,6 +749,9 @@ class TensorQuantizer(nn.Module):
     # ---- forward --------------------------------------------------------------------------------
     def forward(self, inputs):
         """Quantize/calibrate ``inputs`` (reference :1119-1221)."""
+        if isinstance(inputs, (BaseQuantizedTensor, QTensorWrapper)):  # a compressed weight
+            assert self._dequantize, "No dequantization stats in the tensor quantizer."
+            return self.dequantize(inputs)
         if inputs.numel() == 0:
             return inputs
         if self.pre_quant_scale is not None:

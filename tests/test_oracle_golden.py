@@ -236,3 +236,19 @@ def test_awq_clip_oracle_matches_reference(clip_gold):
             best = R.awq_clip_best(total, w_amax, shrinks)
             assert bits_equal(best, t[f"{name}.{n}.best_clip"]), (name, n)
             assert bits_equal(t[f"{name}.{n}.amax"].reshape(best.shape), best), (name, n)
+
+
+def test_mxfp8_oracle_matches_reference_compress():
+    """oracle.mxfp8_quantize reproduces the reference's MXFP8QTensor.quantize (tests/golden/
+    compress.*, written by running the reference's mtq.compress on the CPU) bit for bit."""
+    import json
+
+    from safetensors.torch import load_file
+
+    t = load_file(str(G / "compress.safetensors"))
+    meta = json.loads((G / "compress.json").read_text())
+    for n in meta["mxfp8"]["linears"]:
+        w = t[f"mxfp8.state.{n}.weight"]
+        q, s = R.mxfp8_quantize(w)
+        assert torch.equal(q.view(torch.uint8), t[f"mxfp8.q.{n}"]), n
+        assert torch.equal(s, t[f"mxfp8.scale.{n}"]), n
