@@ -180,6 +180,18 @@ int mtq_qlinear_small_m(const void *x, const void *w, const void *bias, void *y,
                         int64_t N, int64_t K, int dtype, const void *amax, int amax_dtype,
                         int64_t amax_numel, int64_t block, int kind, int num_bits,
                         int is_unsigned, int narrow_range, hipStream_t stream);
+/* The same with a caller-owned workspace for split-K: `ws` (16-byte aligned, at least
+ * mtq_qlinear_small_m_workspace_bytes(M, N, K) bytes, 0 when the shape does not split) holds fp32
+ * partial tiles; the chunks are summed in a fixed order, so results are deterministic.  With
+ * ws == NULL (or mtq_qlinear_small_m) K is not split: a launch has N/16 waves.  The streaming
+ * kernel takes fp32 amax; other amax dtypes and blocks that do not line up with its 128-column
+ * batches (e.g. block 96) run the workgroup-per-tile kernel. */
+size_t mtq_qlinear_small_m_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int mtq_qlinear_small_m_ws(const void *x, const void *w, const void *bias, void *y, int64_t M,
+                           int64_t N, int64_t K, int dtype, const void *amax, int amax_dtype,
+                           int64_t amax_numel, int64_t block, int kind, int num_bits,
+                           int is_unsigned, int narrow_range, void *ws, size_t ws_bytes,
+                           hipStream_t stream);
 
 /* ---- checkpoint export (real-quant packing) ----------------------------------------------
  * export/quant_utils.py:836-938 to_quantized_weight and the qtensor quantize() routines; weights

@@ -774,7 +774,8 @@ at::Tensor qlinear_small_m(const at::Tensor &input, const at::Tensor &weight,
   at::Tensor x = input.contiguous();
   at::Tensor w = weight.contiguous();
   const int64_t M = K ? x.numel() / K : 0;
-  at::Tensor a = amax.contiguous();
+  // fp32 amax: the streaming kernel's layout (a no-op for the calibrators' fp32 amax)
+  at::Tensor a = amax.to(at::kFloat).contiguous();
   TORCH_CHECK(a.device() == x.device(), "qlinear_small_m: amax must be on the input device");
   at::Tensor b;
   if (bias.has_value() && bias->defined()) {
@@ -785,10 +786,13 @@ at::Tensor qlinear_small_m(const at::Tensor &input, const at::Tensor &weight,
   shape.back() = N;
   at::Tensor y = at::empty(shape, x.options());
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  int st = mtq_qlinear_small_m(x.data_ptr(), w.data_ptr(), b.defined() ? b.data_ptr() : nullptr,
-                               y.data_ptr(), M, N, K, dt, a.data_ptr(), checked_dtype(a, "amax"),
-                               a.numel(), block, (int)kind, (int)num_bits, is_unsigned, narrow_range,
-                               cur_stream(x));
+  // split-K partial tiles (fp32) from the caching allocator
+  const size_t wsb = M >= 1 && M <= 16 ? mtq_qlinear_small_m_workspace_bytes(M, N, K) : 0;
+  at::Tensor ws = at::empty({(int64_t)(wsb / sizeof(float))}, x.options().dtype(at::kFloat));
+  int st = mtq_qlinear_small_m_ws(x.data_ptr(), w.data_ptr(), b.defined() ? b.data_ptr() : nullptr,
+                                  y.data_ptr(), M, N, K, dt, a.data_ptr(), checked_dtype(a, "amax"),
+                                  a.numel(), block, (int)kind, (int)num_bits, is_unsigned,
+                                  narrow_range, wsb ? ws.data_ptr() : nullptr, wsb, cur_stream(x));
   check_status(st, "qlinear_small_m");
   return y;
 }
