@@ -319,6 +319,30 @@ int mtq_cpu_fake_e4m3fy(const void *x, void *y, int64_t n, int dtype, const floa
 int mtq_cpu_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtype, float *out,
                         int nthreads);
 
+/* ---- Fused flash attention with softmax-P quant-dequant (MFMA) ----------------------------
+ * Replaces the reference's Triton `_attn_fwd` / `attention()` forward
+ * (modelopt/torch/kernels/common/attention/triton_fa.py:255-516, :1221-1390) as the quantization
+ * plugin dispatches it for `p_bmm_quantizer` (plugins/huggingface.py:125-195): GQA, causal or
+ * not, online softmax over 32-key tiles, P fake-quantised before P.V:
+ *   p_qdq_mode 0: none; 1: FP8 e4m3 per tensor, scale = p_qdq_scale (= amax / 448);
+ *   2: NVFP4 (e2m1, e4m3 scale per 16 keys, global scale p_qdq_scale = amax / (6 * 448)).
+ * Varlen layout of the reference: sequence b's query rows are [b_start_loc[b], + b_seq_len[b])
+ * and its keys [b_start_loc_k[b], + b_seq_len_k[b]) (device int32 arrays of `batch` entries);
+ * element (b, position t, head h, d) of q/k/v/o lives at
+ *   base + b * strides[0|3|6|9] + t * strides[1|4|7|10] + h * strides[2|5|8|11] + d
+ * (element strides, multiples of 16 bytes; d contiguous) -- the reference's flat [tokens, heads, D]
+ * tensors use a zero batch stride, HF's [B, H, S, D] states a non-zero one (no copies).
+ * Causal queries are the last b_seq_len[b] positions of the key span.  Rows past b_seq_len[b]
+ * are not written.  q/k/v/o bf16, f16 or f32 (dtype), 16-byte aligned, head_dim in {16, 32, 64, 96, 128},
+ * num_q_heads % num_kv_heads == 0.  softmax_scale / p_qdq_scale are the Python doubles the
+ * reference passes (its fp32 kernel scalars are derived from them the same way). */
+int mtq_attention_fwd(const void *q, const void *k, const void *v, void *o,
+                      const int32_t *b_start_loc, const int32_t *b_seq_len,
+                      const int32_t *b_start_loc_k, const int32_t *b_seq_len_k, int batch,
+                      int max_len_q, int num_q_heads, int num_kv_heads, int head_dim,
+                      const int64_t *strides, int is_causal, double softmax_scale,
+                      int p_qdq_mode, double p_qdq_scale, int dtype, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,6 +28,7 @@ REPO = HERE.parent
 CSRC = HERE / "csrc"
 INC = REPO / "include"
 OUT = HERE / "modelopt_amd" / "_lib"
+OBJ = HERE / "_obj"  # per-source objects (git- and gpurun-ignored)
 
 ARCH = os.environ.get("MTQ_AMD_ARCH", "gfx950")
 
@@ -52,29 +53,35 @@ def _run(cmd: list[str]) -> None:
 
 
 def build_kernels(force: bool = False) -> Path:
+    """One object per source (compiled in parallel, each rebuilt only when it or a shared header
+    changed), then one link."""
     out = OUT / "libmtq_amd.so"
     srcs = [CSRC / "mtq_kernels.hip", CSRC / "mtq_search.hip", CSRC / "mtq_qlinear.hip", CSRC / "mtq_awq_gemm.hip",
-            CSRC / "mtq_cpu.cpp"]
-    deps = srcs + [CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
-    if force or _stale(out, deps):
+            CSRC / "mtq_attention.hip", CSRC / "mtq_cpu.cpp"]
+    hdrs = [CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
+    OBJ.mkdir(parents=True, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{INC}"]
+    objs, jobs = [], []
+    for src in srcs:
+        obj = OBJ / (src.name + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src, *hdrs]):
+            tmp = obj.with_suffix(".o.tmp")
+            cmd = [_hipcc(), *flags, "-c", str(src), "-o", str(tmp)]
+            print("+", " ".join(cmd), flush=True)
+            jobs.append((subprocess.Popen(cmd), tmp, obj))
+    failed = 0
+    for proc, tmp, obj in jobs:
+        if proc.wait() != 0:
+            failed = proc.returncode
+        else:
+            tmp.replace(obj)
+    if failed:
+        raise subprocess.CalledProcessError(failed, "hipcc")
+    if force or jobs or _stale(out, objs):
         OUT.mkdir(parents=True, exist_ok=True)
         tmp = out.with_suffix(".so.tmp")
-        _run(
-            [
-                _hipcc(),
-                f"--offload-arch={ARCH}",
-                "-O3",
-                "-std=c++17",
-                "-fPIC",
-                "-shared",
-                "-Wall",
-                "-Wno-unused-function",
-                f"-I{INC}",
-                *[str(p) for p in srcs],
-                "-o",
-                str(tmp),
-            ]
-        )
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", *[str(o) for o in objs], "-o", str(tmp)])
         tmp.replace(out)
     return out
 

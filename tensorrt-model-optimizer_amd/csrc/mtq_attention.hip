@@ -1,0 +1,432 @@
+// mtq_attention.hip — fused flash attention with softmax-P fake quant-dequant (gfx950).
+//
+// Reference: modelopt/torch/kernels/common/attention/triton_fa.py `_attn_fwd` (:255-516) as
+// dispatched by `attention()` (:1221-1390) from the quantization plugin's `_triton_qdq_attention`
+// (plugins/huggingface.py:145-195) when `p_bmm_quantizer` is per-tensor FP8 or dynamic NVFP4
+// block 16 on causal attention.  Per query row and per 32-key tile (the kernel's BLOCK_N):
+//
+//     s   = (q . k) * sm_scale * log2(e);  masked keys -> -inf           (:395-403, :194-217)
+//     m'  = max(m, max_tile s);  p = exp2(s - m');  c = exp2(m - m')      (:426-430)
+//     l   = l * c + sum(p);  acc = acc * c                                (:431-432)
+//     p   = qdq(p)            FP8:   e4m3(clamp(p / S, +-448)) * S,  S = amax / 448
+//                             NVFP4: p -> V dtype, per 16 keys e2m1 with an e4m3 block scale,
+//                                    global scale S = amax / (6 * 448)     (:436-451, bmm2_qdq.py)
+//     acc += p . v            FP8/none: p rounded to the V dtype, bf16/f16 MMA, fp32 accumulate
+//                             NVFP4:    fp32 MMA ("ieee" dot, :489)
+//     o   = acc / max(l, 1e-6)                                            (:495)
+// fp32 q/k/v (the reference's Q_IS_FP32 path, :392-393) run both products on
+// v_mfma_f32_32x32x2_f32.
+//
+// The denominator l sums the UNQUANTISED p; the quantised p is relative to the running max of
+// the tiles seen so far, so the result depends on the 32-key tiling -- kept here exactly.
+//
+// Layout (CDNA4-first): a 256-thread workgroup = 4 waves = 128 query rows of one (batch, head);
+// each wave owns 32 rows.  Scores are computed transposed, S^T = K . Q^T with
+// v_mfma_f32_32x32x16_{bf16,f16}, so lane l holds the 16 scores of query (l & 31) for keys
+// crow(j, l >> 5) = (j & 3) + 8 (j >> 2) + 4 (l >> 5): the row max / row sum are 15 in-lane ops
+// and one lane^32 exchange, and the P fragments of P . V come straight out of the score registers
+// (the MMA's k index is permuted to the keys a lane already holds; V is read in the same order).
+// The output is accumulated transposed, O^T = V^T . P^T, so the online-softmax correction is one
+// per-lane scalar.  K and V tiles [32 keys x D] are register-staged into LDS (one copy per
+// workgroup, 16-byte rows padded so ds_read_b128 of the K fragment hits distinct banks), the next
+// tile's global loads issued before the current tile's math.  Workgroups of one KV head are
+// consecutive on one XCD (shared K/V in its L2), the longest causal tiles first.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "mtq_amd.h"
+#include "mtq_device.hpp"
+
+using namespace mtq;
+
+namespace mtq {
+int host_check_launch();
+}
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T> struct AMma;
+template <> struct AMma<__bf16> {
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct AMma<_Float16> {
+  typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+// fp32 q/k/v (the reference's Q_IS_FP32 path, "ieee" dots): both products on v_mfma_f32_32x32x2_f32
+template <> struct AMma<float> {
+  typedef float v8 __attribute__((ext_vector_type(8)));  // unused placeholder
+};
+
+struct AttnArgs {
+  const void *q, *k, *v;
+  void *o;
+  const int32_t *start_q, *len_q, *start_k, *len_k;
+  int64_t qb, qt, qh, kb, kt, kh, vb, vt, vh, ob, ot, oh;  // element strides (batch, token, head)
+  int hkv, group, tiles_q, causal;
+  float qk_scale, p_scale;
+};
+
+constexpr int kThreads = 256, kRowsPerBlock = 128, kKv = 32;
+constexpr float kNegInf = -__builtin_inff();
+
+// key (within the 32-key tile) of score register j of a lane in half hi (C layout of 32x32 MFMA)
+__device__ __forceinline__ int crow(int j, int hi) { return (j & 3) + 8 * (j >> 2) + 4 * hi; }
+
+__device__ __forceinline__ float fp8_rt(float v) {  // e4m3 round trip, RNE (v already clamped)
+  const int p = __builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false);
+  return __builtin_amdgcn_cvt_f32_fp8(p, 0);
+}
+
+// fp4_round_magnitude (kernels/quantization/common/nvfp4_quant.py): nearest E2M1 magnitude,
+// ties to even
+__device__ __forceinline__ float e2m1_mag(float a) {
+  return a <= 0.25f ? 0.f
+       : a < 0.75f  ? 0.5f
+       : a <= 1.25f ? 1.f
+       : a < 1.75f  ? 1.5f
+       : a <= 2.5f  ? 2.f
+       : a < 3.5f   ? 3.f
+       : a <= 5.f   ? 4.f
+                    : 6.f;
+}
+
+template <typename T, int D, int PQ>
+__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
+  typedef typename AMma<T>::v8 v8;
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr bool F32PV = F32 || PQ == 2;  // P . V as an fp32 dot (NVFP4 "ieee", or fp32 P)
+  constexpr int ES = sizeof(T);
+  constexpr int DP = D < 32 ? 32 : D;  // head_dim 16: one 32-wide d block, columns >= D zero
+  constexpr int PITCH = DP * ES + 16;  // LDS row bytes (16-byte pad: conflict-free b128 reads)
+  constexpr int CR = D * ES / 16;     // 16-byte chunks per row
+  constexpr int EC = 16 / ES;         // elements per chunk
+  constexpr int NCH = kKv * CR;      // chunks per tile
+  constexpr int NU = (NCH + kThreads - 1) / kThreads;
+  constexpr int DB = DP / 32;  // 32-wide d blocks of O^T
+  constexpr int QS = D / 16;  // k steps of S^T
+  __shared__ __attribute__((aligned(16))) unsigned char Ks[kKv * PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned char Vs[kKv * PITCH];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 31, hi = lane >> 5;
+
+  // XCD-contiguous remap (bijective): consecutive ids share an XCD, hence its L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int qn = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  int rem = (xcd < rr ? xcd * (qn + 1) : rr * (qn + 1) + (xcd - rr) * qn) + orig / 8;
+  const int tile = a.tiles_q - 1 - rem % a.tiles_q;  // longest causal tiles first
+  rem /= a.tiles_q;
+  const int hg = rem % a.group;
+  rem /= a.group;
+  const int kvh = rem % a.hkv;
+  const int b = rem / a.hkv;
+  const int h = kvh * a.group + hg;
+
+  const int lq = a.len_q[b], lk = a.len_k[b];
+  const int r0 = tile * kRowsPerBlock;
+  if (r0 >= lq) return;  // uniform over the workgroup
+  const int off = lk - lq;  // causal: queries are the last lq positions of the key span
+  const T *Q = reinterpret_cast<const T *>(a.q) + b * a.qb + (int64_t)a.start_q[b] * a.qt + h * a.qh;
+  const T *K = reinterpret_cast<const T *>(a.k) + b * a.kb + (int64_t)a.start_k[b] * a.kt + kvh * a.kh;
+  const T *V = reinterpret_cast<const T *>(a.v) + b * a.vb + (int64_t)a.start_k[b] * a.vt + kvh * a.vh;
+  T *O = reinterpret_cast<T *>(a.o) + b * a.ob + (int64_t)a.start_q[b] * a.ot + h * a.oh;
+
+  const int last = r0 + kRowsPerBlock < lq ? r0 + kRowsPerBlock : lq;
+  int kv_end = a.causal ? off + last : lk;
+  kv_end = kv_end < lk ? kv_end : lk;
+  const int ntiles = kv_end > 0 ? (kv_end + kKv - 1) / kKv : 0;
+
+  const int q0 = r0 + 32 * wave;
+  const bool active = q0 < lq;
+  int w_end = a.causal ? off + (q0 + 32 < lq ? q0 + 32 : lq) : lk;
+  w_end = w_end < lk ? w_end : lk;
+  const int qrow = q0 + fr;
+
+  v8 qf[F32 ? 1 : QS];
+  float qf32[F32 ? D / 2 : 1];
+  if constexpr (F32) {
+#pragma unroll
+    for (int s = 0; s < D / 2; ++s)
+      qf32[s] = qrow < lq ? reinterpret_cast<const float *>(Q)[(int64_t)qrow * a.qt + 2 * s + hi] : 0.f;
+  } else {
+#pragma unroll
+    for (int s = 0; s < QS; ++s) {
+      if (qrow < lq) {
+        qf[s] = *reinterpret_cast<const v8 *>(Q + (int64_t)qrow * a.qt + 16 * s + 8 * hi);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qf[s][i] = (T)0.f;
+      }
+    }
+  }
+
+  f32x16 acc[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[d][e] = 0.f;
+  float m = kNegInf, l = 0.f;
+
+  uint4 kst[NU], vst[NU];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int c = tid + kThreads * u;
+      if (NCH % kThreads == 0 || c < NCH) {
+        const int row = c / CR, col = c - row * CR;
+        const int key = t * kKv + row;
+        if (key < lk) {  // keys past the sequence are zero (0 * garbage could be NaN)
+          kst[u] = *reinterpret_cast<const uint4 *>(K + (int64_t)key * a.kt + col * EC);
+          vst[u] = *reinterpret_cast<const uint4 *>(V + (int64_t)key * a.vt + col * EC);
+        } else {
+          kst[u] = make_uint4(0, 0, 0, 0);
+          vst[u] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int c = tid + kThreads * u;
+      if (NCH % kThreads == 0 || c < NCH) {
+        const int row = c / CR, col = c - row * CR;
+        *reinterpret_cast<uint4 *>(Ks + row * PITCH + col * 16) = kst[u];
+        *reinterpret_cast<uint4 *>(Vs + row * PITCH + col * 16) = vst[u];
+      }
+    }
+  };
+
+  float rs_p = 0.f, six_gs = 0.f, rs_six = 0.f;
+  if (PQ == 1) rs_p = 1.0f / a.p_scale;
+  if (PQ == 2) {
+    six_gs = 6.0f * a.p_scale;
+    rs_six = 1.0f / six_gs;
+  }
+
+  if constexpr (DP != D) {  // V columns D..31 are read by the d block and must be zero
+    for (int i = tid; i < kKv * (DP - D); i += kThreads) {
+      const int row = i / (DP - D), col = D + i % (DP - D);
+      *reinterpret_cast<T *>(Vs + row * PITCH + col * ES) = (T)0.f;
+    }
+  }
+  if (ntiles > 0) {
+    gload(0);
+    swrite();
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);  // in flight across this tile's math
+    const int kv0 = t * kKv;
+    if (active && kv0 < w_end) {
+      // ---- S^T = K . Q^T  (lane: query fr, keys crow(j, hi))
+      f32x16 s;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s[e] = 0.f;
+      if constexpr (F32) {
+#pragma unroll
+        for (int st = 0; st < D / 2; ++st) {
+          const float kv = *reinterpret_cast<const float *>(Ks + fr * PITCH + (2 * st + hi) * 4);
+          s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv, qf32[st], s, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int st = 0; st < QS; ++st) {
+          const v8 kf = *reinterpret_cast<const v8 *>(Ks + fr * PITCH + (16 * st + 8 * hi) * 2);
+          s = AMma<T>::mma(kf, qf[st], s);
+        }
+      }
+      float x[16];
+      float mloc = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int key = kv0 + crow(j, hi);
+        const bool ok = key < lk && (!a.causal || qrow + off >= key);
+        x[j] = ok ? s[j] * a.qk_scale : kNegInf;
+        mloc = fmaxf(mloc, x[j]);
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+      const float mn = fmaxf(m, mloc);
+      const float mu = mn == kNegInf ? 0.f : mn;  // rows with no key yet: p = 0, not NaN
+      float p[16];
+      float ls = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        p[j] = __builtin_amdgcn_exp2f(x[j] - mu);
+        ls += p[j];
+      }
+      ls += __shfl_xor(ls, 32);
+      const float corr = m == mn ? 1.f : __builtin_amdgcn_exp2f(m - mu);
+      l = l * corr + ls;
+#pragma unroll
+      for (int d = 0; d < DB; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[d][e] *= corr;
+      m = mn;
+
+      if (PQ == 1) {
+        // ---- FP8 P qdq: e4m3(clamp(p / S, +-448)) * S  (p >= 0)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          float v = div_rn(p[j], a.p_scale, rs_p);
+          v = v < kE4M3Max ? v : kE4M3Max;
+          p[j] = fp8_rt(v) * a.p_scale;
+        }
+      } else if (PQ == 2) {
+        // ---- NVFP4 P qdq: p -> V dtype -> fp32; per 16 keys (j = 8g..8g+7 of both halves)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) p[j] = Elem<T>::ld(Elem<T>::st(p[j]));
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          float bmax = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) bmax = fmaxf(bmax, p[8 * g + i]);
+          bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+          float s8 = div_rn(bmax, six_gs, rs_six);
+          s8 = s8 < kE4M3Max ? s8 : kE4M3Max;
+          const float sc = fp8_rt(s8) * a.p_scale;
+          const bool zero = sc == 0.f;
+          const float safe = (zero || !(fabsf(sc) < __builtin_inff())) ? 1.f : sc;
+          const float rsafe = 1.0f / safe;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float v = p[8 * g + i];
+            const float qv = e2m1_mag(div_rn(fabsf(v), safe, rsafe)) * safe;
+            p[8 * g + i] = zero ? 0.f : (v >= 0.f ? qv : -qv);
+          }
+        }
+      }
+      if constexpr (F32PV) {
+        // ---- O^T += V^T . P^T in fp32 (v_mfma_f32_32x32x2_f32): step tt pairs key crow(tt, 0)
+        // (lanes 0-31) with crow(tt, 1) (lanes 32-63)
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) {
+          const unsigned char *vrow = Vs + crow(tt, hi) * PITCH;
+#pragma unroll
+          for (int d = 0; d < DB; ++d) {
+            const float vv = Elem<T>::ld(*reinterpret_cast<const T *>(vrow + (32 * d + fr) * ES));
+            acc[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv, p[tt], acc[d], 0, 0, 0);
+          }
+        }
+      } else {
+        // ---- O^T += V^T . P^T with P rounded to the V dtype; k index i of half hi in k-block g
+        // is key crow(8g + i, hi)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          v8 pb;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) pb[i] = Elem<T>::st(p[8 * g + i]);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) {
+            v8 vf;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              vf[i] = *reinterpret_cast<const T *>(Vs + crow(8 * g + i, hi) * PITCH + (32 * d + fr) * 2);
+            acc[d] = AMma<T>::mma(vf, pb, acc[d]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      swrite();
+      __syncthreads();
+    }
+  }
+
+  // ---- o = acc / max(l, 1e-6); lane holds d = 32 d + crow(e, hi) of query row qrow
+  if (active && qrow < lq) {
+    const float den = l > 1e-6f ? l : 1e-6f;
+    const float rden = 1.0f / den;
+    T *orow = O + (int64_t)qrow * a.ot;
+#pragma unroll
+    for (int d = 0; d < DB; ++d)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        if (DP != D && 32 * d + 8 * e4 + 4 * hi >= D) continue;
+        struct alignas(4 * sizeof(T)) Pack {
+          T h[4];
+        } pk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk.h[i] = Elem<T>::st(div_rn(acc[d][4 * e4 + i], den, rden));
+        *reinterpret_cast<Pack *>(orow + 32 * d + 8 * e4 + 4 * hi) = pk;
+      }
+  }
+}
+
+template <typename T, int D>
+int launch_d(const AttnArgs &a, unsigned grid, int mode, hipStream_t stream) {
+  if (mode == 0)
+    attn_fwd_kernel<T, D, 0><<<grid, kThreads, 0, stream>>>(a);
+  else if (mode == 1)
+    attn_fwd_kernel<T, D, 1><<<grid, kThreads, 0, stream>>>(a);
+  else
+    attn_fwd_kernel<T, D, 2><<<grid, kThreads, 0, stream>>>(a);
+  return host_check_launch();
+}
+
+template <typename T>
+int launch_t(const AttnArgs &a, unsigned grid, int d, int mode, hipStream_t stream) {
+  switch (d) {
+  case 16: return launch_d<T, 16>(a, grid, mode, stream);
+  case 32: return launch_d<T, 32>(a, grid, mode, stream);
+  case 64: return launch_d<T, 64>(a, grid, mode, stream);
+  case 96: return launch_d<T, 96>(a, grid, mode, stream);
+  case 128: return launch_d<T, 128>(a, grid, mode, stream);
+  default: return MTQ_ERR_INVALID_ARG;
+  }
+}
+
+inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mtq_attention_fwd(const void *q, const void *k, const void *v, void *o,
+                                 const int32_t *b_start_loc, const int32_t *b_seq_len,
+                                 const int32_t *b_start_loc_k, const int32_t *b_seq_len_k, int batch,
+                                 int max_len_q, int num_q_heads, int num_kv_heads, int head_dim,
+                                 const int64_t *strides, int is_causal, double softmax_scale,
+                                 int p_qdq_mode, double p_qdq_scale, int dtype, hipStream_t stream) {
+  if (!q || !k || !v || !o || !b_start_loc || !b_seq_len || !b_start_loc_k || !b_seq_len_k || !strides)
+    return MTQ_ERR_INVALID_ARG;
+  if (dtype != MTQ_BF16 && dtype != MTQ_F16 && dtype != MTQ_F32) return MTQ_ERR_DTYPE;
+  if (batch < 1 || max_len_q < 0 || num_q_heads < 1 || num_kv_heads < 1 || num_q_heads % num_kv_heads)
+    return MTQ_ERR_INVALID_ARG;
+  if (head_dim != 16 && head_dim != 32 && head_dim != 64 && head_dim != 96 && head_dim != 128)
+    return MTQ_ERR_INVALID_ARG;
+  if (p_qdq_mode < 0 || p_qdq_mode > 2) return MTQ_ERR_FORMAT;
+  if (p_qdq_mode && !(p_qdq_scale > 0.0 && p_qdq_scale < 3.4e38)) return MTQ_ERR_INVALID_ARG;
+  if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return MTQ_ERR_INVALID_ARG;
+  const int64_t ec = dtype == MTQ_F32 ? 4 : 8;  // elements per 16 bytes
+  for (int i = 0; i < 12; ++i)  // 16-byte aligned rows: every stride a multiple of 16 bytes
+    if (strides[i] < 0 || strides[i] % ec) return MTQ_ERR_INVALID_ARG;
+  if (max_len_q == 0) return MTQ_OK;
+  const int64_t tiles_q = (max_len_q + kRowsPerBlock - 1) / kRowsPerBlock;
+  const int64_t blocks = tiles_q * num_q_heads * (int64_t)batch;
+  if (blocks > (int64_t)INT32_MAX) return MTQ_ERR_INVALID_ARG;
+  AttnArgs a;
+  a.q = q, a.k = k, a.v = v, a.o = o;
+  a.start_q = b_start_loc, a.len_q = b_seq_len, a.start_k = b_start_loc_k, a.len_k = b_seq_len_k;
+  a.qb = strides[0], a.qt = strides[1], a.qh = strides[2];
+  a.kb = strides[3], a.kt = strides[4], a.kh = strides[5];
+  a.vb = strides[6], a.vt = strides[7], a.vh = strides[8];
+  a.ob = strides[9], a.ot = strides[10], a.oh = strides[11];
+  a.hkv = num_kv_heads;
+  a.group = num_q_heads / num_kv_heads;
+  a.tiles_q = (int)tiles_q;
+  a.causal = is_causal ? 1 : 0;
+  // triton_fa.py:922 `qk_scale = sm_scale * LOG2E` in Python (double), passed as an fp32 scalar
+  a.qk_scale = (float)(softmax_scale * 1.44269504088896);
+  a.p_scale = (float)p_qdq_scale;
+  if (dtype == MTQ_BF16) return launch_t<__bf16>(a, (unsigned)blocks, head_dim, p_qdq_mode, stream);
+  if (dtype == MTQ_F16) return launch_t<_Float16>(a, (unsigned)blocks, head_dim, p_qdq_mode, stream);
+  return launch_t<float>(a, (unsigned)blocks, head_dim, p_qdq_mode, stream);
+}

@@ -875,6 +875,52 @@ at::Tensor meta_like(const at::Tensor &x) { return at::empty_like(x); }
 
 }  // namespace
 
+// attention_fwd(q, k, v, o (out), b_start_loc, b_seq_len, b_start_loc_k, b_seq_len_k, max_len_q,
+// is_causal, softmax_scale, p_qdq_mode, p_qdq_scale): the reference's Triton flash attention with
+// softmax-P qdq (triton_fa.py:255-516).  q/k/v/o are either the reference's flat [tokens, heads, D]
+// tensors or [B, S, H, D] strided views (e.g. HF's [B, H, S, D] states transposed, no copy); the
+// last dim must be contiguous.  Rows past b_seq_len are left untouched in o.
+void attention_fwd(const at::Tensor &q, const at::Tensor &k, const at::Tensor &v, at::Tensor o,
+                   const at::Tensor &b_start_loc, const at::Tensor &b_seq_len,
+                   const at::Tensor &b_start_loc_k, const at::Tensor &b_seq_len_k, int64_t max_len_q,
+                   bool is_causal, double softmax_scale, int64_t p_qdq_mode, double p_qdq_scale) {
+  check_device(q, "q");
+  const int dt = dtype_code(q.scalar_type());
+  TORCH_CHECK(dt == MTQ_BF16 || dt == MTQ_F16 || dt == MTQ_F32, "attention_fwd: q/k/v must be bf16, fp16 or fp32");
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
+                  o.scalar_type() == q.scalar_type(),
+              "attention_fwd: q, k, v and o must share the dtype");
+  const int64_t nd = q.dim();
+  TORCH_CHECK((nd == 3 || nd == 4) && k.dim() == nd && v.dim() == nd && o.dim() == nd,
+              "attention_fwd: q/k/v/o must all be [tokens, heads, D] or all [B, S, heads, D]");
+  for (const at::Tensor *t : {&q, &k, &v, static_cast<const at::Tensor *>(&o)})
+    TORCH_CHECK(t->is_cuda() && t->device() == q.device() && t->stride(-1) == 1,
+                "attention_fwd: tensors on q's device with a contiguous last dim expected");
+  TORCH_CHECK(o.sizes() == q.sizes() && v.sizes() == k.sizes() && k.size(-1) == q.size(-1),
+              "attention_fwd: shape mismatch");
+  int64_t st[12];
+  const at::Tensor *ts[4] = {&q, &k, &v, &o};
+  for (int i = 0; i < 4; ++i) {
+    st[3 * i] = nd == 4 ? ts[i]->stride(0) : 0;
+    st[3 * i + 1] = ts[i]->stride(nd - 3);
+    st[3 * i + 2] = ts[i]->stride(nd - 2);
+  }
+  const int64_t batch = b_seq_len.numel();
+  auto meta = [&](const at::Tensor &t, const char *name) {
+    TORCH_CHECK(t.numel() == batch, "attention_fwd: ", name, " must have one entry per sequence");
+    return t.to(q.device(), at::kInt).contiguous();
+  };
+  at::Tensor sl = meta(b_start_loc, "b_start_loc"), ln = meta(b_seq_len, "b_seq_len");
+  at::Tensor slk = meta(b_start_loc_k, "b_start_loc_k"), lnk = meta(b_seq_len_k, "b_seq_len_k");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(q.device());
+  check_status(mtq_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                 sl.data_ptr<int32_t>(), ln.data_ptr<int32_t>(), slk.data_ptr<int32_t>(),
+                                 lnk.data_ptr<int32_t>(), (int)batch, (int)max_len_q, (int)q.size(-2),
+                                 (int)k.size(-2), (int)q.size(-1), st, is_causal ? 1 : 0, softmax_scale,
+                                 (int)p_qdq_mode, p_qdq_scale, dt, cur_stream(q)),
+               "attention_fwd");
+}
+
 TORCH_LIBRARY(modelopt_amd, m) {
   m.def("quantize_op(Tensor input, Tensor amax, int num_bits, int exponent_bits, bool unsigned, "
         "bool narrow_range) -> Tensor");
@@ -918,6 +964,9 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "bool narrow_range, bool round_candidate_amax) -> Tensor");
   m.def("awq_clip_search(Tensor weight, Tensor x, Tensor w_amax, Tensor shrinks, Tensor(a!) loss, "
         "int block, int num_bits, bool unsigned, bool narrow_range, bool accumulate) -> ()");
+  m.def("attention_fwd(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor b_start_loc, Tensor b_seq_len, "
+        "Tensor b_start_loc_k, Tensor b_seq_len_k, int max_len_q, bool is_causal, float softmax_scale, "
+        "int p_qdq_mode, float p_qdq_scale) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
@@ -950,6 +999,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("nvfp4_fp8_scale_sweep", &nvfp4_fp8_scale_sweep);
   m.impl("mse_sweep", &mse_sweep);
   m.impl("awq_clip_search", &awq_clip_search);
+  m.impl("attention_fwd", &attention_fwd);
 }
 
 // the reference's "cpu" registration (tensor_quant.py:252-256), on the host kernels

@@ -299,9 +299,12 @@ class _QuantAttention(QuantModule):
     ``q/k/v_bmm_quantizer`` fake-quantise the query / key / value states handed to the attention
     function (after RoPE and the KV-cache update, as the reference); they are per-tensor HIP
     passes that read the transposed ``[B, H, S, D]`` states in place (no ``.contiguous()`` copy).
-    ``p_bmm_quantizer`` fake-quantises the softmax probabilities: the reference fuses that into a
-    Triton flash-attention kernel (causal) or wraps ``F.softmax`` in the eager attention
-    (non-causal); here both cases run the module's eager attention with the quantised softmax."""
+    ``p_bmm_quantizer`` fake-quantises the softmax probabilities as the reference dispatches it
+    (:125-251): per-tensor FP8 or dynamic NVFP4 block 16 on causal attention run the fused MFMA
+    flash attention with the P qdq inside (``mtq_attention_fwd``, csrc/mtq_attention.hip; the
+    reference's Triton ``_attn_fwd``), non-causal attention wraps ``F.softmax`` of the original
+    attention function, and any other P format leaves the attention unquantised (the reference
+    hands those to the optional ``kitchen`` package, which is not part of this path)."""
 
     def _setup(self):
         self.q_bmm_quantizer = TensorQuantizer()
@@ -318,7 +321,42 @@ class _QuantAttention(QuantModule):
         mod = inspect.getmodule(attn_cls)
         return getattr(mod, "ALL_ATTENTION_FUNCTIONS", None) is not None
 
-    def _eager_p_qdq_attention(self, eager_fn, query_states, key_states, value_states, *args, **kwargs):
+    def _p_qdq_mode(self) -> str | None:
+        """reference :125-143: "fp8" (per-tensor E4M3), "nvfp4" (dynamic, block 16) or None."""
+        pq = self.p_bmm_quantizer
+        if not pq.is_enabled:
+            return None
+        if pq.is_fp8:
+            return "fp8"
+        if pq.is_nvfp4_dynamic and (pq.block_sizes or {}).get(-1, None) == 16:
+            return "nvfp4"
+        return None
+
+    def _fused_qdq_attention(self, p_qdq, query_states, key_states, value_states, **kwargs):
+        """reference ``_triton_qdq_attention`` :145-195 on the MFMA kernel: the calibrated (or
+        user-set) per-tensor amax of ``p_bmm_quantizer`` is the P scale, 1.0 without one."""
+        from ...kernels.common.attention import attention_forward, validate_attention_envelope
+
+        attention_mask = kwargs.pop("attention_mask", None)
+        validate_attention_envelope(self, query_states, key_states, attention_mask, **kwargs)
+        p_qdq_amax = None
+        pq_amax = getattr(self.p_bmm_quantizer, "_amax", None)
+        if pq_amax is not None:
+            if pq_amax.numel() != 1:
+                raise NotImplementedError(
+                    "p_bmm_quantizer via the Triton attention kernel only supports a "
+                    f"per-tensor (scalar) amax, got shape {tuple(pq_amax.shape)}."
+                )
+            p_qdq_amax = float(pq_amax)
+        scaling = kwargs.get("scaling")
+        if scaling is None:
+            scaling = query_states.shape[-1] ** -0.5
+        return attention_forward(self, query_states, key_states, value_states, attention_mask, scaling,
+                                 p_qdq=p_qdq, p_qdq_amax=p_qdq_amax)
+
+    def _eager_p_qdq_attention(self, original, query_states, key_states, value_states, **kwargs):
+        """reference :197-218: ``F.softmax`` replaced by ``p_bmm_quantizer(softmax(...))`` inside
+        the original attention function (an SDPA-fused softmax is unaffected, as there)."""
         pq = self.p_bmm_quantizer
         orig_softmax = torch.nn.functional.softmax
 
@@ -326,16 +364,22 @@ class _QuantAttention(QuantModule):
             return pq(orig_softmax(*s_args, **s_kwargs))
 
         with _replace_function(torch.nn.functional, "softmax", _quantized_softmax):
-            return eager_fn(self, query_states, key_states, value_states, *args, **kwargs)
+            return original(self, query_states, key_states, value_states, **kwargs)
 
     @staticmethod
-    def _quantized_attention(original_attention_interface, eager_fn, self, query_states, key_states,
+    def _quantized_attention(original_attention_interface, self, query_states, key_states,
                              value_states, *args, **kwargs):
         query_states = self.q_bmm_quantizer(query_states)
         key_states = self.k_bmm_quantizer(key_states)
         value_states = self.v_bmm_quantizer(value_states)
-        if self.p_bmm_quantizer.is_enabled:
-            return self._eager_p_qdq_attention(eager_fn, query_states, key_states, value_states, *args, **kwargs)
+        p_qdq = self._p_qdq_mode()
+        if p_qdq is not None:
+            if args:  # the attention interface passes attention_mask positionally (reference :240-241)
+                kwargs["attention_mask"] = args[0]
+            if kwargs.get("is_causal") is False or getattr(self, "is_causal", True) is False:
+                return self._eager_p_qdq_attention(original_attention_interface, query_states, key_states,
+                                                   value_states, **kwargs)
+            return self._fused_qdq_attention(p_qdq, query_states, key_states, value_states, **kwargs)
         return original_attention_interface(self, query_states, key_states, value_states, *args, **kwargs)
 
     def forward(self, *args, **kwargs):
@@ -355,9 +399,7 @@ class _QuantAttention(QuantModule):
             original = eager_fn
         else:
             original = module.ALL_ATTENTION_FUNCTIONS[impl]
-        if self.p_bmm_quantizer.is_enabled and eager_fn is None:
-            raise NotImplementedError(f"p_bmm_quantizer needs the eager attention of {module}")
-        patch_fn = functools.partial(self._quantized_attention, original, eager_fn)
+        patch_fn = functools.partial(self._quantized_attention, original)
         registry = module.ALL_ATTENTION_FUNCTIONS
         had_local = (not eager) and impl in registry._local_mapping
         if eager:

@@ -1,0 +1,228 @@
+"""Fused flash attention with softmax-P qdq (csrc/mtq_attention.hip, ``mtq_attention_fwd``) on the
+GPU vs (a) the reference's own Triton kernel outputs (tests/golden/attention.*), (b) the oracle
+(oracle/attention_ref.py, pinned to those goldens) at larger shapes, (c) a plain fp32 PyTorch
+attention without P qdq, and (d) the quantization plugin end to end on a tiny Llama.
+
+Tolerance (stated once, used everywhere): scores and P . V are fp32 MFMA sums in a different
+order than the reference's, and p = exp2(.) comes from v_exp_f32 (1 ulp); a p element that sits
+on an FP8 / E2M1 rounding boundary can therefore land one quantum away, which moves the output
+by at most quantum * |v| / l.  Bound: |err| <= 2e-2 + 2e-2 |want| on every element, and the
+mean |err| at the bf16 rounding level (<= 2e-3)."""
+
+import json
+import math
+from pathlib import Path
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from oracle import attention_ref as A
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+META = json.loads((G / "attention.json").read_text())
+
+
+def _close(got, want, what=""):
+    got, want = got.float().cpu(), want.float().cpu()
+    assert torch.isfinite(got).all(), what
+    err = (got - want).abs()
+    bound = 2e-2 + 2e-2 * want.abs()
+    assert bool((err <= bound).all()), f"{what}: max err {float(err.max())}"
+    assert float(err.mean()) <= 2e-3, f"{what}: mean err {float(err.mean())}"
+    return err
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return load_file(str(G / "attention.safetensors"))
+
+
+def _kw(mt, dev):
+    b, lq, lk = mt["batch"], mt["lens_q"], mt["lens_k"]
+    sq, sk = max(lq), max(lk)
+    kw = dict(b_start_loc=(torch.arange(b) * sq).int().to(dev), b_seq_len=torch.tensor(lq).int().to(dev),
+              max_input_len=sq, is_causal=mt["causal"], softmax_scale=mt["d"] ** -0.5,
+              b_start_loc_k=(torch.arange(b) * sk).int().to(dev), b_seq_len_k=torch.tensor(lk).int().to(dev))
+    if mt["p_qdq"]:
+        kw["p_qdq"] = mt["p_qdq"]
+        if mt["amax"] is not None:
+            kw["p_qdq_amax"] = mt["amax"]
+    return kw
+
+
+@pytest.mark.parametrize("name", sorted(META))
+def test_kernel_matches_reference_triton_kernel(gpu, gold, name):
+    from modelopt_amd.torch.kernels.common.attention import attention
+
+    mt = META[name]
+    q, k, v = (gold[f"{name}.{t}"].to(gpu) for t in "qkv")
+    o = attention(q, k, v, **_kw(mt, gpu))
+    valid = torch.zeros(q.shape[0], dtype=torch.bool)
+    s = max(mt["lens_q"])
+    for i, n in enumerate(mt["lens_q"]):
+        valid[i * s: i * s + n] = True
+    got = torch.where(valid[:, None, None], o.cpu(), torch.zeros((), dtype=o.dtype))
+    err = _close(got, gold[f"{name}.o"], name)
+    # most elements are bit-identical to the reference's own kernel
+    assert float((err == 0).float().mean()) >= 0.5, float((err == 0).float().mean())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("p_qdq,amax", [(None, 1.0), ("fp8", 1.0), ("fp8", 0.37), ("nvfp4", 1.0), ("nvfp4", 0.8)])
+def test_kernel_matches_oracle(gpu, dtype, d, p_qdq, amax):
+    """Multi-block shapes: 2 sequences (300 and 161 tokens), GQA 8:2, several 128-row tiles."""
+    from modelopt_amd.torch.kernels.common.attention import attention
+
+    g = torch.Generator().manual_seed(d + (7 if p_qdq else 0))
+    lens, s, hq, hkv = [300, 161], 300, 8, 2
+    q = (torch.randn(2 * s, hq, d, generator=g) * 1.5).to(dtype)
+    k = (torch.randn(2 * s, hkv, d, generator=g) * 1.5).to(dtype)
+    v = torch.randn(2 * s, hkv, d, generator=g).to(dtype)
+    start, ln = torch.tensor([0, s]).int(), torch.tensor(lens).int()
+    kw = dict(is_causal=True, softmax_scale=d ** -0.5, p_qdq=p_qdq)
+    if p_qdq:
+        kw["p_qdq_amax"] = amax
+    o = attention(q.to(gpu), k.to(gpu), v.to(gpu), start.to(gpu), ln.to(gpu), s, **kw)
+    want = A.attention_fwd(q, k, v, start, ln, **kw)
+    got = o.cpu()
+    got[lens[1] + s:] = 0
+    _close(got, want, f"{dtype} d{d} {p_qdq} {amax}")
+
+
+@pytest.mark.parametrize("d", [16, 32, 64, 96, 128])
+def test_unquantized_matches_fp32_attention(gpu, d):
+    """No P qdq: the kernel vs plain fp32 PyTorch attention (P kept in fp32, so the bound is the
+    bf16 rounding of P before P . V plus the output rounding)."""
+    from modelopt_amd.torch.kernels.common.attention import attention
+
+    g = torch.Generator().manual_seed(d)
+    b, s, hq, hkv = 3, 200, 4, 4
+    q = torch.randn(b * s, hq, d, generator=g).bfloat16()
+    k = torch.randn(b * s, hkv, d, generator=g).bfloat16()
+    v = torch.randn(b * s, hkv, d, generator=g).bfloat16()
+    start, ln = (torch.arange(b) * s).int(), torch.full((b,), s).int()
+    o = attention(q.to(gpu), k.to(gpu), v.to(gpu), start.to(gpu), ln.to(gpu), s, is_causal=True)
+    qf, kf, vf = (t.float().view(b, s, -1, d).transpose(1, 2).to(gpu) for t in (q, k, v))
+    ref = torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, is_causal=True)
+    ref = ref.transpose(1, 2).reshape(b * s, hq, d)
+    torch.testing.assert_close(o.float(), ref, rtol=2e-2, atol=2e-2)
+    assert float((o.float() - ref).abs().mean()) < 3e-3
+
+
+def test_decode_attends_to_whole_cache(gpu):
+    """Single-token queries (is_causal False): every cached key is visible (reference decode)."""
+    from modelopt_amd.torch.kernels.common.attention import attention
+
+    g = torch.Generator().manual_seed(3)
+    b, sk, hq, hkv, d = 4, 77, 8, 2, 128
+    q = torch.randn(b, hq, d, generator=g).bfloat16()
+    k = torch.randn(b * sk, hkv, d, generator=g).bfloat16()
+    v = torch.randn(b * sk, hkv, d, generator=g).bfloat16()
+    lk = torch.tensor([77, 1, 40, 64]).int()
+    kw = dict(b_start_loc=torch.arange(b).int(), b_seq_len=torch.ones(b).int(), is_causal=False,
+              b_start_loc_k=(torch.arange(b) * sk).int(), b_seq_len_k=lk, p_qdq="fp8")
+    want = A.attention_fwd(q, k, v, **kw)
+    kwg = {n: (t.to(gpu) if torch.is_tensor(t) else t) for n, t in kw.items()}
+    o = attention(q.to(gpu), k.to(gpu), v.to(gpu), max_input_len=1, **kwg)
+    _close(o, want, "decode")
+
+
+def test_hf_strided_path_equals_flat_path(gpu):
+    """attention_forward reads HF's [B, H, S, D] states through their strides and writes
+    [B, S, H, D]: bit-identical to the flat reference-layout call on contiguous copies."""
+    from modelopt_amd.torch.kernels.common.attention import attention, attention_forward
+
+    g = torch.Generator().manual_seed(11)
+    b, s, hq, hkv, d = 2, 90, 4, 2, 64
+    qp = torch.randn(b, s, hq * d, generator=g).bfloat16().to(gpu)
+    kp = torch.randn(b, s, hkv * d, generator=g).bfloat16().to(gpu)
+    vp = torch.randn(b, s, hkv * d, generator=g).bfloat16().to(gpu)
+    q = qp.view(b, s, hq, d).transpose(1, 2)  # HF layout: views of the projection outputs
+    k = kp.view(b, s, hkv, d).transpose(1, 2)
+    v = vp.view(b, s, hkv, d).transpose(1, 2)
+    mask = torch.ones(b, s, dtype=torch.long, device=gpu)
+    mask[1, 60:] = 0
+    out, _ = attention_forward(None, q, k, v, mask, d ** -0.5, p_qdq="nvfp4", p_qdq_amax=0.9)
+    flat = attention(qp.reshape(b * s, hq, d), kp.reshape(b * s, hkv, d), vp.reshape(b * s, hkv, d),
+                     torch.tensor([0, s], device=gpu).int(), torch.tensor([s, 60], device=gpu).int(), s,
+                     softmax_scale=d ** -0.5, p_qdq="nvfp4", p_qdq_amax=0.9).view(b, s, hq, d)
+    assert torch.equal(out[0], flat[0]) and torch.equal(out[1, :60], flat[1, :60])
+    assert bool((out[1, 60:] == 0).all())  # padding rows zeroed, as the reference wrapper
+
+
+def _tiny_llama(gpu, dtype=torch.bfloat16, hidden=128):
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=256, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=64, max_position_embeddings=128,
+                      architectures=["LlamaForCausalLM"])
+    torch.manual_seed(80)
+    return LlamaForCausalLM(cfg).eval().to(dtype).to(gpu)
+
+
+@pytest.mark.parametrize("dtype,hidden", [(torch.bfloat16, 128), (torch.float32, 64)])
+@pytest.mark.parametrize("fmt", ["fp8", "nvfp4"])
+def test_plugin_routes_p_bmm_through_fused_kernel(gpu, fmt, dtype, hidden):
+    """mtq.quantize with a P quantizer on a causal Llama: the attention output equals the
+    restatement projections -> RoPE -> q/k/v qdq -> oracle flash attention with the P qdq
+    (reference plugins/huggingface.py:145-195); the P quantizer collects no amax during
+    calibration (the kernel consumes P), so its scale is the default amax 1.0."""
+    import copy
+
+    import modelopt_amd.torch.quantization as mtq
+
+    m = _tiny_llama(gpu, dtype, hidden)
+    cfg = copy.deepcopy(mtq.FP8_DEFAULT_CFG)
+    p_cfg = ({"num_bits": (4, 3), "axis": None} if fmt == "fp8" else
+             {"num_bits": (2, 1), "block_sizes": {-1: 16, "type": "dynamic", "scale_bits": (4, 3)}, "axis": None})
+    cfg["quant_cfg"] = cfg["quant_cfg"] + [
+        {"quantizer_name": "*[kv]_bmm_quantizer", "cfg": {"num_bits": (4, 3), "axis": None}},
+        {"quantizer_name": "*p_bmm_quantizer", "cfg": p_cfg},
+    ]
+    ids = torch.randint(0, 64, (2, 2, 24), generator=torch.Generator().manual_seed(5)).to(gpu)
+    mtq.quantize(m, cfg, lambda mm: [mm(b) for b in ids])
+    att = m.model.layers[0].self_attn
+    assert att._p_qdq_mode() == fmt
+    assert getattr(att.p_bmm_quantizer, "_amax", None) is None
+    h = torch.randn(1, 40, hidden, generator=torch.Generator().manual_seed(6)).to(dtype).to(gpu)
+    pos = torch.arange(40, device=gpu)[None]
+    pe = m.model.rotary_emb(h, pos)
+    with torch.no_grad():
+        out, _ = att(h, position_embeddings=pe, attention_mask=None)
+        from transformers.models.llama.modeling_llama import apply_rotary_pos_emb
+
+        hs = (1, 40, -1, att.head_dim)
+        q = att.q_proj(h).view(hs).transpose(1, 2)
+        k = att.k_proj(h).view(hs).transpose(1, 2)
+        v = att.v_proj(h).view(hs).transpose(1, 2)
+        q, k = apply_rotary_pos_emb(q, k, *pe)
+        k, v = att.k_bmm_quantizer(k), att.v_bmm_quantizer(v)
+        flat = lambda t: t[0].transpose(0, 1).contiguous().cpu()  # noqa: E731  [S, H, D]
+        o = A.attention_fwd(flat(q), flat(k), flat(v), torch.tensor([0]), torch.tensor([40]),
+                            softmax_scale=att.scaling, p_qdq=fmt)
+        ref = att.o_proj(o.reshape(1, 40, -1).to(gpu))
+    _close(out, ref, f"plugin {fmt}")
+
+
+def test_plugin_non_causal_uses_eager_softmax_wrapper(gpu):
+    """Non-causal attention keeps the reference's eager path: F.softmax wrapped by the P
+    quantizer inside the original attention function (reference :197-218, :245-248)."""
+    import copy
+
+    import modelopt_amd.torch.quantization as mtq
+
+    m = _tiny_llama(gpu)
+    m.config._attn_implementation = "eager"
+    cfg = copy.deepcopy(mtq.FP8_DEFAULT_CFG)
+    cfg["quant_cfg"] = cfg["quant_cfg"] + [
+        {"quantizer_name": "*p_bmm_quantizer", "cfg": {"num_bits": (4, 3), "axis": None}}]
+    ids = torch.randint(0, 64, (1, 2, 16), generator=torch.Generator().manual_seed(5)).to(gpu)
+    for layer in m.model.layers:
+        layer.self_attn.is_causal = False
+    mtq.quantize(m, cfg, lambda mm: [mm(b) for b in ids])
+    att = m.model.layers[0].self_attn
+    amax = float(att.p_bmm_quantizer.amax)  # calibrated through the wrapped softmax
+    assert 0 < amax <= 1.0 and math.isfinite(amax)

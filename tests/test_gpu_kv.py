@@ -121,34 +121,5 @@ def test_per_tensor_qdq_reads_strided_states_in_place(gpu, dtype):
     assert torch.equal(yi.contiguous(), quantize_op(x.contiguous(), amax, 8, 0, False, False))
 
 
-def test_p_bmm_quantizer_eager_softmax(gpu):
-    """p_bmm_quantizer: P = fake_quant(softmax(Q K^T * scaling)) before P V (reference :200-218)."""
-    import modelopt_amd.torch.quantization as mtq
-
-    m = _tiny().to(gpu)
-    cfg = _cfg(mtq, "qkv_fp8")
-    cfg["quant_cfg"] = cfg["quant_cfg"] + [{"quantizer_name": "*p_bmm_quantizer", "cfg": {"num_bits": (4, 3), "axis": None}}]
-    ids = torch.randint(0, 32, (2, 2, 16), generator=torch.Generator().manual_seed(5)).to(gpu)
-    mtq.quantize(m, cfg, lambda mm: [mm(b) for b in ids])
-    att = m.model.layers[0].self_attn
-    assert att.p_bmm_quantizer.is_enabled and float(att.p_bmm_quantizer.amax) <= 1.0
-    h = torch.randn(1, 12, 64, device=gpu)
-    pos = torch.arange(12, device=gpu)[None]
-    pe = m.model.rotary_emb(h, pos)
-    with torch.no_grad():
-        out, _ = att(h, position_embeddings=pe, attention_mask=None)
-        # the same attention restated: projections, RoPE, q/k/v/P qdq with the calibrated amax
-        from transformers.models.llama.modeling_llama import apply_rotary_pos_emb, repeat_kv
-
-        hs = (1, 12, -1, att.head_dim)
-        q = att.q_proj(h).view(hs).transpose(1, 2)
-        k = att.k_proj(h).view(hs).transpose(1, 2)
-        v = att.v_proj(h).view(hs).transpose(1, 2)
-        q, k = apply_rotary_pos_emb(q, k, *pe)
-        fq = lambda t, qz: R.fp8_eager(t.cpu(), qz.amax.cpu()).to(gpu)  # noqa: E731
-        q, k, v = fq(q, att.q_bmm_quantizer), fq(k, att.k_bmm_quantizer), fq(v, att.v_bmm_quantizer)
-        k, v = repeat_kv(k, att.num_key_value_groups), repeat_kv(v, att.num_key_value_groups)
-        p = torch.softmax(torch.matmul(q, k.transpose(2, 3)) * att.scaling, dim=-1, dtype=torch.float32).to(q.dtype)
-        p = fq(p, att.p_bmm_quantizer)
-        ref = att.o_proj(torch.matmul(p, v).transpose(1, 2).reshape(1, 12, -1))
-    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)
+# p_bmm_quantizer (softmax-P qdq): tests/test_gpu_attention.py -- the causal path runs the fused
+# MFMA flash attention as the reference dispatches it (plugins/huggingface.py:236-251).
