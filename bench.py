@@ -168,6 +168,19 @@ def kernel_suite(ops, xs, steps, warmup):
     return res
 
 
+def attention_suite(iters: int = 20):
+    """The fused flash attention with softmax-P qdq (mtq_attention_fwd) on a Llama-3-8B
+    calibration batch (16 x 512 tokens, 32 / 8 heads, D 128, bf16, causal): MFMA TFLOP/s per P
+    mode vs the 2.5 PF dense bf16 peak, beside torch SDPA without P qdq."""
+    from scripts import bench_attention  # noqa: PLC0415
+
+    r = bench_attention.measure(iters=iters)
+    peak = r["peak_tflops_bf16_dense"]
+    for v in list(r["modes"].values()) + [r["sdpa_no_qdq"], r["eager_fp8_p"]]:
+        v["frac_mfma_peak"] = round(v["tflops"] / peak, 4)
+    return r
+
+
 def host_cpu_info():
     """Physical cores of the host (unique (package, core) pairs in /proc/cpuinfo), the CPUs this
     process may run on, and torch's intra-op thread count."""
@@ -378,6 +391,7 @@ def main():
     }
     if rank == 0 and not args.no_suite:
         out["kernels"] = kernel_suite(ops, xs, args.steps, args.warmup)
+        out["attention_p_qdq"] = attention_suite()
     if not args.no_ptq:
         from scripts import ptq_llama  # noqa: PLC0415
 

@@ -39,15 +39,9 @@ def timed(fn, iters):
     return e0.elapsed_time(e1) / iters
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--out", default=None)
-    args = ap.parse_args()
+def measure(iters=20, batch=16, seq=512):
     dev = torch.device("cuda")
-    B, S, HQ, HKV, D = args.batch, args.seq, 32, 8, 128
+    B, S, HQ, HKV, D = batch, seq, 32, 8, 128
     g = torch.Generator(device=dev).manual_seed(0)
     q = torch.randn(B * S, HQ, D, device=dev, generator=g).bfloat16()
     k = torch.randn(B * S, HKV, D, device=dev, generator=g).bfloat16()
@@ -58,13 +52,13 @@ def main():
     res = {"shape": {"batch": B, "seq": S, "hq": HQ, "hkv": HKV, "d": D, "dtype": "bf16", "causal": True},
            "flop_per_launch": flop, "peak_tflops_bf16_dense": 2500.0, "modes": {}}
     for mode in (None, "fp8", "nvfp4"):
-        ms = timed(lambda: attention(q, k, v, start, lens, S, p_qdq=mode), args.iters)
+        ms = timed(lambda: attention(q, k, v, start, lens, S, p_qdq=mode), iters)
         res["modes"][str(mode)] = {"ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}
     # torch SDPA, no P qdq (HF's default attention)
     qs = q.view(B, S, HQ, D).transpose(1, 2)
     ks = k.view(B, S, HKV, D).transpose(1, 2).repeat_interleave(HQ // HKV, dim=1)
     vs = v.view(B, S, HKV, D).transpose(1, 2).repeat_interleave(HQ // HKV, dim=1)
-    ms = timed(lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=True), args.iters)
+    ms = timed(lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=True), iters)
     res["sdpa_no_qdq"] = {"ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}
     # the unfused eager path a P quantizer otherwise needs (scores materialised)
     amax = torch.tensor(1.0, device=dev)
@@ -75,8 +69,19 @@ def main():
         p = torch.softmax(s, dim=-1, dtype=torch.float32).to(qs.dtype)
         return torch.matmul(fp8_fake_quant(p, amax), vs)
 
-    ms = timed(eager, max(3, args.iters // 4))
+    ms = timed(eager, max(3, iters // 4))
     res["eager_fp8_p"] = {"ms": round(ms, 4), "tflops": round(flop / ms / 1e9, 1)}
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    res = measure(args.iters, args.batch, args.seq)
     print(json.dumps(res, indent=1))
     if args.out:
         Path(args.out).write_text(json.dumps(res, indent=1))

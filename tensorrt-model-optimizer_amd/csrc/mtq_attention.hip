@@ -27,13 +27,15 @@
 // and one lane^32 exchange, and the P fragments of P . V come straight out of the score registers
 // (the MMA's k index is permuted to the keys a lane already holds; V is read in the same order).
 // The output is accumulated transposed, O^T = V^T . P^T, so the online-softmax correction is one
-// per-lane scalar.  K and V tiles [32 keys x D] are register-staged into LDS (one copy per
-// workgroup, 16-byte rows padded so ds_read_b128 of the K fragment hits distinct banks), the next
-// tile's global loads issued before the current tile's math.  Workgroups of one KV head are
+// per-lane scalar.  K and V [64 keys x D] (two softmax tiles) are register-staged into LDS per
+// barrier pair (one copy per workgroup; K rows padded so ds_read_b128 of the K fragment hits
+// distinct banks, V rows padded for conflict-free ds_read_b64_tr_b16, which delivers the V^T
+// fragments transposed), the next stage's global loads issued before the current stage's math.  Workgroups of one KV head are
 // consecutive on one XCD (shared K/V in its L2), the longest causal tiles first.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "mtq_amd.h"
 #include "mtq_device.hpp"
@@ -76,6 +78,8 @@ struct AttnArgs {
 };
 
 constexpr int kThreads = 256, kRowsPerBlock = 128, kKv = 32;
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
 constexpr float kNegInf = -__builtin_inff();
 
 // key (within the 32-key tile) of score register j of a lane in half hi (C layout of 32x32 MFMA)
@@ -99,22 +103,33 @@ __device__ __forceinline__ float e2m1_mag(float a) {
                     : 6.f;
 }
 
-template <typename T, int D, int PQ>
-__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
+template <typename T, int D, int PQ, int kStage>  // kStage: keys staged in LDS per barrier pair
+__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
   typedef typename AMma<T>::v8 v8;
   constexpr bool F32 = sizeof(T) == 4;
-  constexpr bool F32PV = F32 || PQ == 2;  // P . V as an fp32 dot (NVFP4 "ieee", or fp32 P)
+  // P . V of NVFP4 is an fp32 ("ieee") dot in the reference.  bf16: P (fp32) is split exactly
+  // into three bf16 terms p = p1 + p2 + p3 (8 significant bits each) and V . p1 + V . p2 + V . p3
+  // runs on the bf16 MFMA -- every product exact, fp32 accumulation, 3 MFMAs of k = 16 instead of
+  // 8 v_mfma_f32_32x32x2_f32.  f16 (whose exponent range cannot hold the small terms) and fp32
+  // q/k/v keep the fp32 MFMA.
+  constexpr bool SPLIT3 = PQ == 2 && !F32 && __is_same(T, __bf16);
+  constexpr bool F32PV = F32 || (PQ == 2 && !SPLIT3);
   constexpr int ES = sizeof(T);
   constexpr int DP = D < 32 ? 32 : D;  // head_dim 16: one 32-wide d block, columns >= D zero
-  constexpr int PITCH = DP * ES + 16;  // LDS row bytes (16-byte pad: conflict-free b128 reads)
+  constexpr int PITCH = DP * ES + 16;  // K row bytes (16-byte pad: conflict-free b128 reads)
+  // V rows for ds_read_b64_tr_b16: a 32-lane half reads 4 rows x 16 dwords, conflict-free when
+  // the row stride is 16 or 48 dwords mod 64
+  // (the fp32 P . V path reads V per element instead and keeps the K pitch: its two lane halves
+  // read rows 4 apart, which the tr pitch would put on the same banks)
+  constexpr int VPITCH = F32PV ? PITCH : DP * 2 + 4 * ((16 - (DP / 2) % 32 + 32) % 32);
   constexpr int CR = D * ES / 16;     // 16-byte chunks per row
   constexpr int EC = 16 / ES;         // elements per chunk
-  constexpr int NCH = kKv * CR;      // chunks per tile
+  constexpr int NCH = kStage * CR;   // chunks per stage
   constexpr int NU = (NCH + kThreads - 1) / kThreads;
   constexpr int DB = DP / 32;  // 32-wide d blocks of O^T
   constexpr int QS = D / 16;  // k steps of S^T
-  __shared__ __attribute__((aligned(16))) unsigned char Ks[kKv * PITCH];
-  __shared__ __attribute__((aligned(16))) unsigned char Vs[kKv * PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned char Ks[kStage * PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned char Vs[kStage * VPITCH];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 31, hi = lane >> 5;
 
@@ -142,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
   const int last = r0 + kRowsPerBlock < lq ? r0 + kRowsPerBlock : lq;
   int kv_end = a.causal ? off + last : lk;
   kv_end = kv_end < lk ? kv_end : lk;
-  const int ntiles = kv_end > 0 ? (kv_end + kKv - 1) / kKv : 0;
+  const int nstages = kv_end > 0 ? (kv_end + kStage - 1) / kStage : 0;
 
   const int q0 = r0 + 32 * wave;
   const bool active = q0 < lq;
@@ -182,7 +197,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
       const int c = tid + kThreads * u;
       if (NCH % kThreads == 0 || c < NCH) {
         const int row = c / CR, col = c - row * CR;
-        const int key = t * kKv + row;
+        const int key = t * kStage + row;
         if (key < lk) {  // keys past the sequence are zero (0 * garbage could be NaN)
           kst[u] = *reinterpret_cast<const uint4 *>(K + (int64_t)key * a.kt + col * EC);
           vst[u] = *reinterpret_cast<const uint4 *>(V + (int64_t)key * a.vt + col * EC);
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
       if (NCH % kThreads == 0 || c < NCH) {
         const int row = c / CR, col = c - row * CR;
         *reinterpret_cast<uint4 *>(Ks + row * PITCH + col * 16) = kst[u];
-        *reinterpret_cast<uint4 *>(Vs + row * PITCH + col * 16) = vst[u];
+        *reinterpret_cast<uint4 *>(Vs + row * VPITCH + col * 16) = vst[u];
       }
     }
   };
@@ -213,19 +228,31 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
   }
 
   if constexpr (DP != D) {  // V columns D..31 are read by the d block and must be zero
-    for (int i = tid; i < kKv * (DP - D); i += kThreads) {
+    for (int i = tid; i < kStage * (DP - D); i += kThreads) {
       const int row = i / (DP - D), col = D + i % (DP - D);
-      *reinterpret_cast<T *>(Vs + row * PITCH + col * ES) = (T)0.f;
+      *reinterpret_cast<T *>(Vs + row * VPITCH + col * ES) = (T)0.f;
     }
   }
-  if (ntiles > 0) {
+  // ds_read_b64_tr_b16 address of this lane (T10): lane 4q+p of 16-lane group G supplies row
+  // 4 (G >> 1) + q, columns 16 (G & 1) + 4p .. +3 of a [keys][d] block; lane (G, i) receives
+  // column 16 (G & 1) + i = fr of those 4 rows = the V^T fragment elements of its half
+  const int trq = (lane & 15) >> 2, trp = lane & 3, trg = lane >> 4;
+  const int tr_off = (4 * (trg >> 1) + trq) * VPITCH + (16 * (trg & 1) + 4 * trp) * 2;
+
+  if (nstages > 0) {
     gload(0);
     swrite();
   }
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) gload(t + 1);  // in flight across this tile's math
-    const int kv0 = t * kKv;
+  for (int t = 0; t < nstages; ++t) {
+    if (t + 1 < nstages) gload(t + 1);  // in flight across this stage's math
+#pragma unroll
+    for (int sub = 0; sub < kStage / kKv; ++sub) {
+    const int kv0 = t * kStage + sub * kKv;
+    const unsigned char *const Kt = Ks + sub * kKv * PITCH;
+    const unsigned char *const Vt = Vs + sub * kKv * VPITCH;
+    // wave-uniform: a tile with no masked (row, key) pair skips the mask arithmetic
+    const bool need_mask = kv0 + kKv > lk || (a.causal && kv0 + kKv - 1 > q0 + off);
     if (active && kv0 < w_end) {
       // ---- S^T = K . Q^T  (lane: query fr, keys crow(j, hi))
       f32x16 s;
@@ -234,24 +261,32 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
       if constexpr (F32) {
 #pragma unroll
         for (int st = 0; st < D / 2; ++st) {
-          const float kv = *reinterpret_cast<const float *>(Ks + fr * PITCH + (2 * st + hi) * 4);
+          const float kv = *reinterpret_cast<const float *>(Kt + fr * PITCH + (2 * st + hi) * 4);
           s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv, qf32[st], s, 0, 0, 0);
         }
       } else {
 #pragma unroll
         for (int st = 0; st < QS; ++st) {
-          const v8 kf = *reinterpret_cast<const v8 *>(Ks + fr * PITCH + (16 * st + 8 * hi) * 2);
+          const v8 kf = *reinterpret_cast<const v8 *>(Kt + fr * PITCH + (16 * st + 8 * hi) * 2);
           s = AMma<T>::mma(kf, qf[st], s);
         }
       }
       float x[16];
       float mloc = kNegInf;
+      if (need_mask) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int key = kv0 + crow(j, hi);
-        const bool ok = key < lk && (!a.causal || qrow + off >= key);
-        x[j] = ok ? s[j] * a.qk_scale : kNegInf;
-        mloc = fmaxf(mloc, x[j]);
+        for (int j = 0; j < 16; ++j) {
+          const int key = kv0 + crow(j, hi);
+          const bool ok = key < lk && (!a.causal || qrow + off >= key);
+          x[j] = ok ? s[j] * a.qk_scale : kNegInf;
+          mloc = fmaxf(mloc, x[j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          x[j] = s[j] * a.qk_scale;
+          mloc = fmaxf(mloc, x[j]);
+        }
       }
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
       const float mn = fmaxf(m, mloc);
@@ -309,7 +344,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
         // (lanes 0-31) with crow(tt, 1) (lanes 32-63)
 #pragma unroll
         for (int tt = 0; tt < 16; ++tt) {
-          const unsigned char *vrow = Vs + crow(tt, hi) * PITCH;
+          const unsigned char *vrow = Vt + crow(tt, hi) * VPITCH;
 #pragma unroll
           for (int d = 0; d < DB; ++d) {
             const float vv = Elem<T>::ld(*reinterpret_cast<const T *>(vrow + (32 * d + fr) * ES));
@@ -321,22 +356,38 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
         // is key crow(8g + i, hi)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          v8 pb;
+          v8 pb, pb2, pb3;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) pb[i] = Elem<T>::st(p[8 * g + i]);
+          for (int i = 0; i < 8; ++i) {
+            pb[i] = Elem<T>::st(p[8 * g + i]);
+            if constexpr (SPLIT3) {
+              const float r1 = p[8 * g + i] - Elem<T>::ld(pb[i]);  // exact
+              pb2[i] = Elem<T>::st(r1);
+              pb3[i] = Elem<T>::st(r1 - Elem<T>::ld(pb2[i]));     // exact
+            }
+          }
 #pragma unroll
           for (int d = 0; d < DB; ++d) {
-            v8 vf;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-              vf[i] = *reinterpret_cast<const T *>(Vs + crow(8 * g + i, hi) * PITCH + (32 * d + fr) * 2);
+            // elements 0-3: keys 16g + 4hi + 0..3, elements 4-7: keys 16g + 8 + 4hi + 0..3
+            const unsigned char *base = Vt + tr_off + 16 * g * VPITCH + 64 * d;
+            const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) v4s *)(base));
+            const v4s up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) v4s *)(base + 8 * VPITCH));
+            const v8s w = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+            const v8 vf = __builtin_bit_cast(v8, w);
+            if constexpr (SPLIT3) {  // smallest terms first
+              acc[d] = AMma<T>::mma(vf, pb3, acc[d]);
+              acc[d] = AMma<T>::mma(vf, pb2, acc[d]);
+            }
             acc[d] = AMma<T>::mma(vf, pb, acc[d]);
           }
         }
       }
     }
+    }
     __syncthreads();
-    if (t + 1 < ntiles) {
+    if (t + 1 < nstages) {
       swrite();
       __syncthreads();
     }
@@ -362,14 +413,31 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+int stage_keys() {  // A/B switch for measurements: MTQ_AMD_ATTN_STAGE=32|64 (default 64)
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("MTQ_AMD_ATTN_STAGE");
+    v = (e && atoi(e) == 32) ? 32 : 64;
+  }
+  return v;
+}
+
+template <typename T, int D, int ST>
+void launch_st(const AttnArgs &a, unsigned grid, int mode, hipStream_t stream) {
+  if (mode == 0)
+    attn_fwd_kernel<T, D, 0, ST><<<grid, kThreads, 0, stream>>>(a);
+  else if (mode == 1)
+    attn_fwd_kernel<T, D, 1, ST><<<grid, kThreads, 0, stream>>>(a);
+  else
+    attn_fwd_kernel<T, D, 2, ST><<<grid, kThreads, 0, stream>>>(a);
+}
+
 template <typename T, int D>
 int launch_d(const AttnArgs &a, unsigned grid, int mode, hipStream_t stream) {
-  if (mode == 0)
-    attn_fwd_kernel<T, D, 0><<<grid, kThreads, 0, stream>>>(a);
-  else if (mode == 1)
-    attn_fwd_kernel<T, D, 1><<<grid, kThreads, 0, stream>>>(a);
+  if (stage_keys() == 64)
+    launch_st<T, D, 64>(a, grid, mode, stream);
   else
-    attn_fwd_kernel<T, D, 2><<<grid, kThreads, 0, stream>>>(a);
+    launch_st<T, D, 32>(a, grid, mode, stream);
   return host_check_launch();
 }
 

@@ -65,8 +65,13 @@ def test_kernel_matches_reference_triton_kernel(gpu, gold, name):
         valid[i * s: i * s + n] = True
     got = torch.where(valid[:, None, None], o.cpu(), torch.zeros((), dtype=o.dtype))
     err = _close(got, gold[f"{name}.o"], name)
-    # most elements are bit-identical to the reference's own kernel
-    assert float((err == 0).float().mean()) >= 0.5, float((err == 0).float().mean())
+    # against the reference's own kernel the bound is much tighter (measured on MI355X,
+    # scripts/attn_err_stats.py: >= 99.91 % of the elements bit-identical, 5 of 9 cases entirely,
+    # the rest within 0.92 ulp of the output dtype)
+    want = gold[f"{name}.o"].float()
+    ulp = torch.finfo(gold[f"{name}.o"].dtype).eps * torch.maximum(want.abs(), torch.tensor(2.0 ** -6))
+    assert bool((err <= ulp).all()), float((err / ulp).max())
+    assert float((err == 0).float().mean()) >= 0.998, float((err == 0).float().mean())
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])

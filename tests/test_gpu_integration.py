@@ -62,6 +62,27 @@ def test_integration_ctypes_stub_on_device(gpu, dtype):
     assert torch.equal(q.cpu(), R.export_nvfp4(w, bs, s2))
 
 
+@pytest.mark.parametrize("p_qdq", [None, "fp8", "nvfp4"])
+def test_integration_attention_stub_on_device(gpu, p_qdq):
+    """The attention binding of INTEGRATION.md §2c on device tensors == the torch op path and
+    the oracle (oracle/attention_ref.py) within the fused-attention tolerance."""
+    from modelopt_amd.torch.kernels.common.attention import attention
+    from oracle import attention_ref as A
+
+    stub = _integration_stub()
+    g = torch.Generator().manual_seed(17)
+    q = torch.randn(2 * 70, 4, 64, generator=g).bfloat16()
+    k = torch.randn(2 * 70, 2, 64, generator=g).bfloat16()
+    v = torch.randn(2 * 70, 2, 64, generator=g).bfloat16()
+    st, ln = torch.tensor([0, 70]).int(), torch.tensor([70, 41]).int()
+    o = stub["attention_fwd"](q.to(gpu), k.to(gpu), v.to(gpu), st.to(gpu), ln.to(gpu), 70, p_qdq=p_qdq)
+    ref = attention(q.to(gpu), k.to(gpu), v.to(gpu), st.to(gpu), ln.to(gpu), 70, p_qdq=p_qdq)
+    valid = torch.cat([torch.ones(70), torch.ones(41), torch.zeros(29)]).bool()
+    assert torch.equal(o[valid.to(gpu)], ref[valid.to(gpu)])
+    want = A.attention_fwd(q, k, v, st, ln, p_qdq=p_qdq)
+    torch.testing.assert_close(o.cpu()[valid].float(), want[valid].float(), rtol=2e-2, atol=2e-2)
+
+
 def test_integration_stub_reports_errors(gpu):
     stub = _integration_stub()
     x = torch.randn(8, device=gpu, dtype=torch.bfloat16)
