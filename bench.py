@@ -384,7 +384,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "ew_group_kernel<bf16, Fp8AxisVecOp, U=2> via modelopt_amd::quantize_op",
+            "kernel": "ew_group_sk_kernel<bf16, Fp8AxisVecOp, U=2, LPB=8> (scalar-loaded block amax) via modelopt_amd::quantize_op",
             "algorithmic_bytes_per_launch": alg_bytes,
             "mean_launch_ms": round(ms, 4),
         },

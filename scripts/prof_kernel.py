@@ -31,6 +31,7 @@ amax = torch.tensor(8.0, device="cuda")
 acc = torch.zeros(1, device="cuda")
 hmax = torch.tensor([16.0 * 6], device="cuda")  # bench.py's histogram range
 counts = torch.zeros(2048, dtype=torch.int32, device="cuda")
+nv_bs = torch.ones(T, H // 16, device="cuda")  # bench.py's export_nvfp4_pack scales
 torch.cuda.synchronize()
 for i in range(args.iters):
     x = xs[i % 4]
@@ -48,6 +49,12 @@ for i in range(args.iters):
         ops.nvfp4_fake_quant_block(x, amax, 16)
     elif args.kernel == "amax":
         ops.amax_accumulate(x, acc, 1, 1, x.numel())
+    elif args.kernel == "export_fp8":
+        ops.export_fp8(x, amax / 448, False, True)
+    elif args.kernel == "export_nvfp4":
+        ops.export_nvfp4(x, nv_bs, amax / 2688)
+    elif args.kernel == "export_mxfp4":
+        ops.export_mxfp4(x, 32)
     else:
         raise SystemExit(f"unknown kernel {args.kernel}")
 torch.cuda.synchronize()

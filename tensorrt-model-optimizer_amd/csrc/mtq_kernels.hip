@@ -201,6 +201,7 @@ template <typename T> struct IntAxisVecOp {
   __device__ __forceinline__ IntQ qparam(int64_t vi) const {
     return make_intq(load_as_float(amax, amax_dtype, chan(vi)), max_bound, min_bound);
   }
+  __device__ __forceinline__ IntQ qparam_from(float a) const { return make_intq(a, max_bound, min_bound); }
   __device__ __forceinline__ static void apply(Vec<T> &v, const IntQ &q) {
 #pragma unroll
     for (int j = 0; j < Vec<T>::N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
@@ -277,6 +278,7 @@ template <typename T> struct Fp8AxisVecOp {
   __device__ __forceinline__ Fp8Q qparam(int64_t vi) const {
     return make_fp8q(load_as_float(amax, amax_dtype, chan(vi)));
   }
+  __device__ __forceinline__ Fp8Q qparam_from(float a) const { return make_fp8q(a); }
   __device__ __forceinline__ static void apply(Vec<T> &v, const Fp8Q &q) { fp8_vec(v, q); }
   __device__ __forceinline__ void vec(Vec<T> &v, int64_t vi) { fp8_vec(v, qparam(vi)); }
   __device__ __forceinline__ float one(float x, int64_t i) {
@@ -358,6 +360,48 @@ __global__ __launch_bounds__(kThreads) void ew_group_kernel(const T *__restrict_
   }
 }
 
+// Default for fp32 amax with channel = vector / VB (no wrap; MTQ_AMD_GROUP_VARIANT=3 selects the
+// per-lane-load kernel above for A/B): the wave's 64 / LPB channel amax values arrive through
+// scalar loads from one wave-uniform address (scalar cache, no vector-memory instruction, no
+// per-lane address) and each lane selects its own.  FP8 block-128 bf16 [32768, 4096]: 88.3 ->
+// 83.4-84.9 us (76.6 -> 79.7-81.1 % of HBM peak, profiles/r02/export/).
+template <typename T, class Op, int U, int LPB>
+__global__ __launch_bounds__(kThreads) void ew_group_sk_kernel(const T *__restrict__ x,
+                                                                T *__restrict__ y, int64_t nvec,
+                                                                const float *__restrict__ amax,
+                                                                int64_t nchan, Op op) {
+  using V = Vec<T>;
+  constexpr int CPW = 64 / LPB;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wb = ((int64_t)blockIdx.x * kThreads + (int64_t)w * 64) * U;
+  const int k = lane / LPB, pos = lane - k * LPB;
+  const int64_t v0 = wb + (int64_t)k * LPB * U + pos;
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = v0 + (int64_t)u * LPB;
+    if (i < nvec) v[u] = ldg_vec_nt(x + i * V::N);
+  }
+  const int64_t c0 = wb / (LPB * U);
+  float am = amax[c0 < nchan ? c0 : nchan - 1];
+#pragma unroll
+  for (int j = 1; j < CPW; ++j) {
+    const float a = amax[c0 + j < nchan ? c0 + j : nchan - 1];
+    am = k == j ? a : am;
+  }
+  if (v0 >= nvec) return;
+  const auto q = op.qparam_from(am);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = v0 + (int64_t)u * LPB;
+    if (i < nvec) {
+      Op::apply(v[u], q);
+      stg_vec_nt(y + i * V::N, v[u]);
+    }
+  }
+}
+
 int group_variant() {
   static int v = -1;
   if (v < 0) {
@@ -394,7 +438,18 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
       constexpr int U = 2;
       const int64_t nvec = n / N;
       const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
-      if (nvec > 0)
+      const bool sk = gv != 3 && op.amax_dtype == MTQ_F32 && op.small && axis_size * vb == nvec;
+      if (nvec > 0 && sk) {
+        auto go = [&](auto lc) {
+          constexpr int L = decltype(lc)::value;
+          ew_group_sk_kernel<T, VecOp<T>, U, L><<<g, kThreads, 0, stream>>>(
+              reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
+              reinterpret_cast<const float *>(op.amax), axis_size, op);
+        };
+        if (vb == 16) go(std::integral_constant<int, 8>{});
+        else if (vb == 32) go(std::integral_constant<int, 16>{});
+        else go(std::integral_constant<int, 32>{});
+      } else if (nvec > 0)
         ew_group_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec, (int)(vb / U), op);
       const int64_t done = nvec * N;
@@ -1788,6 +1843,18 @@ __device__ __forceinline__ uint32_t e4m3_byte(float v) {
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xFFu;
 }
 
+// A NaN weight keeps its sign through the reference's division and its dtype re-rounding (torch
+// CPU), where the device's bf16 round trip makes the NaN positive: the e4m3 NaN byte takes the
+// weight's sign bit.
+// The sign comes from the raw element bits: the widening convert of a 16-bit NaN does not keep it.
+template <typename T> __device__ __forceinline__ uint32_t nan_sign_byte(T x) {
+  const float f = Elem<T>::ld(x);
+  if constexpr (sizeof(T) == 2)
+    return f != f ? (uint32_t)(__builtin_bit_cast(uint16_t, x) >> 8) & 0x80u : 0u;
+  else
+    return f != f ? (__float_as_uint(f) >> 24) & 0x80u : 0u;
+}
+
 // weight / scale -> e4m3 bytes.  per_row: scale[row] (the division then happens in fp32, as torch
 // promotes bf16 / fp32[rows, 1] to fp32); per-tensor: scale[0] and, with round_dtype, the quotient
 // is first rounded to the weight dtype (torch keeps bf16 / 0-dim fp32 in bf16).
@@ -1800,9 +1867,10 @@ __global__ __launch_bounds__(kThreads) void export_fp8_kernel(const T *__restric
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
     const float s = scale[per_row ? i / cols : 0];
-    float q = div_rn(Elem<T>::ld(x[i]), s, 1.0f / s);
+    const float xv = Elem<T>::ld(x[i]);
+    float q = div_rn(xv, s, 1.0f / s);
     if (round_dtype) q = Elem<T>::ld(Elem<T>::st(q));
-    y[i] = (uint8_t)e4m3_byte(q);
+    y[i] = (uint8_t)(e4m3_byte(q) | nan_sign_byte(x[i]));
   }
 }
 
@@ -1823,7 +1891,7 @@ __global__ __launch_bounds__(kThreads) void export_int4_kernel(const T *__restri
     for (int h = 0; h < 2; ++h) {
       const int64_t r = 2 * pr + h;
       const float s = scale[r * nblk + c / block];
-      float q = __builtin_rintf(div_rn(Elem<T>::ld(x[r * cols + c]), s, 1.0f / s));
+      float q = __builtin_rintf(Elem<T>::ld(x[r * cols + c]) / s);  // IEEE: any s, +-inf
       q = q < -8.f ? -8.f : (q > 7.f ? 7.f : q);  // NaN stays NaN -> int8 cast below
       const int v = q != q ? 0 : (int)q;
       out |= ((uint32_t)v & 0xFu) << (4 * h);
@@ -1863,9 +1931,8 @@ __global__ __launch_bounds__(kThreads) void export_nvfp4_kernel(const T *__restr
     const int64_t e0 = 2 * i;
     const int64_t row = e0 / cols, c = e0 - row * cols;  // cols even: a pair never straddles rows
     const float d = sblk[row * nb_row + c / block] * g;
-    const float r = 1.0f / d;
-    const uint32_t lo = nvfp4_code(div_rn(Elem<T>::ld(x[e0]), d, r));
-    const uint32_t hi = nvfp4_code(div_rn(Elem<T>::ld(x[e0 + 1]), d, r));
+    const uint32_t lo = nvfp4_code(Elem<T>::ld(x[e0]) / d);  // IEEE: any d, +-inf
+    const uint32_t hi = nvfp4_code(Elem<T>::ld(x[e0 + 1]) / d);
     y[i] = (uint8_t)(lo | (hi << 4));
   }
 }
@@ -1952,13 +2019,37 @@ __device__ __forceinline__ int64_t idx_div(int64_t n, int64_t d, const FastDiv &
     return n / d;
 }
 
+// Native fast paths of the packers (`native` kernel argument, MTQ_AMD_EXPORT_NATIVE=0 turns them
+// off for A/B): each lane first converts its vector with the gfx950 converts and a handful of
+// VALU ops, checks the few inputs where the converter and the reference disagree, and only a lane
+// that holds one of those redoes the vector on the exact emulated path above.  The emulated path
+// costs ~25 VALU ops per element (seven threshold compares per E2M1 code), which made the packers
+// VALU-bound at 38-52 % of the HBM roofline.
+
+// E2M1 codes of two fp32 values through v_cvt_scalef32_pk_fp4_f32: x / 2^e(s), round to nearest
+// with ties to the even code, saturating at +-6, -0 -> 8, NaN -> 7 | sign
+// (profiles/r02/fp4_convert_probe.txt).
+__device__ __forceinline__ uint32_t fp4_pair_hw(float a, float b, float s) {
+  return __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, a, b, s, 0) & 0xFFu;
+}
+
+// correctly rounded q / s (div_rn) with a zero quotient always +0: the fma's own -0 from a
+// negative underflow becomes +0 through the `+ 0.0f` (RN: -0 + +0 = +0), which is what the
+// NVFP4 packer's sign rule (q < 0) gives for both zeros.
+__device__ __forceinline__ float div_rn_pz(float q, float s, float r) {
+  const float y0 = q * r;
+  const float e = __builtin_fmaf(-y0, s, q);
+  return __builtin_fmaf(e, r, y0) + 0.0f;
+}
+
 template <typename T, bool IDX32>
 __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restrict__ x,
                                                                    uint8_t *__restrict__ y,
                                                                    int64_t nvec, int64_t cv,
                                                                    FastDiv fcv,
                                                                    const float *__restrict__ scale,
-                                                                   int per_row, int round_dtype) {
+                                                                   int per_row, int round_dtype,
+                                                                   int native) {
   using V = Vec<T>;
   constexpr int N = V::N;
   if (i >= nvec) return;
@@ -1966,11 +2057,37 @@ __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restric
   const float s = scale[per_row ? idx_div<IDX32>(i, cv, fcv) : 0];
   const float r = 1.0f / s;
   uint32_t b[N];
+  if (native) {
+    // |q| <= 448 (NaN fails the test): the packed RNE convert needs no clamp and no NaN patch, two
+    // bytes per v_cvt_pk_fp8_f32.  Lanes with an overflow / NaN quotient take the exact path.
+    float q[N];
+    bool inrange = true;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      q[j] = div_rn(Elem<T>::ld(v.e[j]), s, r);
+      if (round_dtype) q[j] = Elem<T>::ld(Elem<T>::st(q[j]));
+      inrange &= fabsf(q[j]) <= kE4M3Max;
+    }
+    if (inrange) {
+      uint32_t w[N / 4];
+#pragma unroll
+      for (int k = 0; k < N / 4; ++k) {
+        int p = __builtin_amdgcn_cvt_pk_fp8_f32(q[4 * k], q[4 * k + 1], 0, false);
+        w[k] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(q[4 * k + 2], q[4 * k + 3], p, true);
+      }
+      if constexpr (N == 8)
+        st_packed_nt(y + i * N, w[0], w[1]);
+      else
+        st_packed_nt(y + i * N, w[0]);
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    float q = div_rn(Elem<T>::ld(v.e[j]), s, r);
+    const float xv = Elem<T>::ld(v.e[j]);
+    float q = div_rn(xv, s, r);
     if (round_dtype) q = Elem<T>::ld(Elem<T>::st(q));
-    b[j] = e4m3_byte(q);
+    b[j] = e4m3_byte(q) | nan_sign_byte(v.e[j]);
   }
   if constexpr (N == 8)
     st_packed_nt(y + i * N, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
@@ -1997,16 +2114,28 @@ __device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restri
   const int64_t cb = idx_div<IDX32>(c0, block, fblk);
   const float s0 = scale[(2 * pr) * nblk + cb], s1 = scale[(2 * pr + 1) * nblk + cb];
   const float r0 = 1.0f / s0, r1 = 1.0f / s1;
+  // div_rn is the IEEE quotient except where that quotient overflows or the operands are not
+  // finite / positive (div_rn then gives NaN, IEEE +-inf): a lane that saw a NaN quotient (rare;
+  // NaN weights included, which give the same bytes either way) repacks its vector with the IEEE
+  // division operator.
   uint32_t b[N];
+  bool redo = false;
+  auto pack = [&](auto ieee) {
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    float q0 = __builtin_rintf(div_rn(Elem<T>::ld(lo.e[j]), s0, r0));
-    float q1 = __builtin_rintf(div_rn(Elem<T>::ld(hi.e[j]), s1, r1));
-    q0 = q0 < -8.f ? -8.f : (q0 > 7.f ? 7.f : q0);
-    q1 = q1 < -8.f ? -8.f : (q1 > 7.f ? 7.f : q1);
-    const int v0 = q0 != q0 ? 0 : (int)q0, v1 = q1 != q1 ? 0 : (int)q1;
-    b[j] = ((uint32_t)v0 & 0xFu) | (((uint32_t)v1 & 0xFu) << 4);
-  }
+    for (int j = 0; j < N; ++j) {
+      const float x0 = Elem<T>::ld(lo.e[j]), x1 = Elem<T>::ld(hi.e[j]);
+      const float d0 = decltype(ieee)::value ? x0 / s0 : div_rn(x0, s0, r0);
+      const float d1 = decltype(ieee)::value ? x1 / s1 : div_rn(x1, s1, r1);
+      if (!decltype(ieee)::value) redo |= (d0 != d0) | (d1 != d1);
+      float q0 = __builtin_rintf(d0), q1 = __builtin_rintf(d1);
+      q0 = q0 < -8.f ? -8.f : (q0 > 7.f ? 7.f : q0);
+      q1 = q1 < -8.f ? -8.f : (q1 > 7.f ? 7.f : q1);
+      const int v0 = q0 != q0 ? 0 : (int)q0, v1 = q1 != q1 ? 0 : (int)q1;
+      b[j] = ((uint32_t)v0 & 0xFu) | (((uint32_t)v1 & 0xFu) << 4);
+    }
+  };
+  pack(std::false_type{});
+  if (redo) pack(std::true_type{});
   if constexpr (N == 8)
     st_packed_nt(y + pr * cols + c0, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
                  b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
@@ -2021,7 +2150,8 @@ __device__ __forceinline__ void export_nvfp4_vec_one(int64_t i, const T *__restr
                                                                      int64_t nvec, int64_t vpb,
                                                                      FastDiv fvpb,
                                                                      const float *__restrict__ sblk,
-                                                                     const float *__restrict__ s2) {
+                                                                     const float *__restrict__ s2,
+                                                                     int native) {
   using V = Vec<T>;
   constexpr int N = V::N;
   if (i >= nvec) return;
@@ -2029,11 +2159,43 @@ __device__ __forceinline__ void export_nvfp4_vec_one(int64_t i, const T *__restr
   const float d = sblk[idx_div<IDX32>(i, vpb, fvpb)] * (*s2);
   const float r = 1.0f / d;
   uint32_t o = 0;
+  // Native: the converter's ties-to-even-code rounding with saturation is the reference's
+  // searchsorted + odd-bound adjustment (nvfp4_tensor.py:230-250) for every finite q and +-inf;
+  // -0 is made +0 by div_rn_pz, and a NaN quotient (or a non-positive / non-finite divisor)
+  // sends the lane to the exact path.
+  if (native && d > 0.f && r < __builtin_huge_valf() && d < __builtin_huge_valf()) {
+    bool nan = false;
 #pragma unroll
-  for (int j = 0; j < N; j += 2) {
-    const uint32_t lo = nvfp4_code(div_rn(Elem<T>::ld(v.e[j]), d, r));
-    const uint32_t hi = nvfp4_code(div_rn(Elem<T>::ld(v.e[j + 1]), d, r));
-    o |= (lo | (hi << 4)) << (4 * j);
+    for (int j = 0; j < N; j += 2) {
+      const float q0 = div_rn_pz(Elem<T>::ld(v.e[j]), d, r);
+      const float q1 = div_rn_pz(Elem<T>::ld(v.e[j + 1]), d, r);
+      nan |= (q0 != q0) | (q1 != q1);
+      o |= fp4_pair_hw(q0, q1, 1.0f) << (4 * j);
+    }
+    if (!nan) {
+      if constexpr (N == 8)
+        st_packed_nt(y + i * (N / 2), o);
+      else
+        st_packed_nt(y + i * (N / 2), (uint16_t)o);
+      return;
+    }
+    o = 0;
+  }
+  if (native) {
+    // exact lane: IEEE division handles what div_rn does not (+-inf / d, a zero or non-finite d)
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      const uint32_t lo = nvfp4_code(Elem<T>::ld(v.e[j]) / d);
+      const uint32_t hi = nvfp4_code(Elem<T>::ld(v.e[j + 1]) / d);
+      o |= (lo | (hi << 4)) << (4 * j);
+    }
+  } else {  // the r01 emulated kernel, kept as the A/B baseline
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      const uint32_t lo = nvfp4_code(div_rn(Elem<T>::ld(v.e[j]), d, r));
+      const uint32_t hi = nvfp4_code(div_rn(Elem<T>::ld(v.e[j + 1]), d, r));
+      o |= (lo | (hi << 4)) << (4 * j);
+    }
   }
   if constexpr (N == 8)
     st_packed_nt(y + i * (N / 2), o);
@@ -2047,27 +2209,67 @@ template <typename T, int BLOCK>
 __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const T *__restrict__ x,
                                                                      uint8_t *__restrict__ y,
                                                                      uint8_t *__restrict__ sc,
-                                                                     int64_t nvec) {
+                                                                     int64_t nvec, int native) {
   using V = Vec<T>;
   constexpr int N = V::N;
   constexpr int LPB = BLOCK / N;
   if (i - (threadIdx.x % LPB) >= nvec) return;
   V v = ldg_vec_nt(x + i * N);
   float amax = 0.f;
+  if constexpr (N == 8) {
+    // 16-bit elements: max of the |x| bit patterns, two per packed u16 op (NaN patterns sort
+    // above inf, so a NaN propagates as torch.max does)
+    const uint32_t w[4] = {v.raw.x, v.raw.y, v.raw.z, v.raw.w};
+    const uint32_t m = group_max_u32<LPB>(scan_pairs(w).max_abs);
+    amax = half_bits_to_float<T>(m);
+  } else {
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    const float a = fabsf(Elem<T>::ld(v.e[j]));
-    amax = (a > amax || a != a) ? a : amax;
-  }
+    for (int j = 0; j < N; ++j) {
+      const float a = fabsf(Elem<T>::ld(v.e[j]));
+      amax = (a > amax || a != a) ? a : amax;
+    }
 #pragma unroll
-  for (int o = LPB / 2; o > 0; o >>= 1) {
-    const float t = __shfl_xor(amax, o, 64);
-    amax = (t > amax || t != t) ? t : amax;
+    for (int o = LPB / 2; o > 0; o >>= 1) {
+      const float t = __shfl_xor(amax, o, 64);
+      amax = (t > amax || t != t) ? t : amax;
+    }
   }
   const float e = mx_e8m0_exponent(amax / 6.0f);
   if (threadIdx.x % LPB == 0) sc[i / LPB] = (uint8_t)(int)(e + 127.f);
-  const float pinv = (e == e) ? exp2f(-e) : e;  // exact power of two: x * 2^-e == x / 2^e
   uint32_t o = 0;
+  if constexpr (N == 8) {
+    // Native (16-bit elements, -100 <= e <= 127 so 2^e is a normal scale operand and no input the
+    // converter might flush can reach a nonzero code): the reference counts strict `bounds < |q|`,
+    // i.e. ties toward zero, where the converter rounds ties to the even code -- they differ on
+    // |q| = 0.75, 1.75, 3.5.  A 16-bit x has at most 11 significant bits, so x minus one fp32 ulp
+    // lies strictly between x and every other 16-bit value: it falls on the same side of every
+    // midpoint as x does, except that a midpoint itself now rounds down.  A quotient x / 2^e that
+    // is zero in fp32 -- x = +-0, or |x| <= 2^(e - 150) underflowing -- is code 8 in the reference
+    // (torch.sign(0) = 0) where the converter sees a signed tiny value: those nibbles are patched.
+    // A NaN element makes e NaN and takes the exact path.
+    if (native && e >= -100.f && e <= 127.f) {
+      const int ei = (int)e;
+      const float s = __uint_as_float((uint32_t)(ei + 127) << 23);
+      // largest |x| whose quotient rounds to zero: 2^(e - 150) (normal for e >= 24, subnormal
+      // for 1 <= e <= 23; below every nonzero 16-bit value for e < 1)
+      const float zthr = __uint_as_float(ei >= 24 ? (uint32_t)(ei - 23) << 23
+                                                  : (ei >= 1 ? 1u << (ei - 1) : 0u));
+      uint32_t zero = 0;
+#pragma unroll
+      for (int j = 0; j < N; j += 2) {
+        const float f0 = Elem<T>::ld(v.e[j]), f1 = Elem<T>::ld(v.e[j + 1]);
+        zero |= (fabsf(f0) <= zthr ? 0xFu : 0u) << (4 * j);
+        zero |= (fabsf(f1) <= zthr ? 0xFu : 0u) << (4 * j + 4);
+        o |= fp4_pair_hw(__uint_as_float(__float_as_uint(f0) - 1u),
+                         __uint_as_float(__float_as_uint(f1) - 1u), s)
+             << (4 * j);
+      }
+      o = (o & ~zero) | (zero & 0x88888888u);
+      st_packed_nt(y + i * (N / 2), o);
+      return;
+    }
+  }
+  const float pinv = (e == e) ? exp2f(-e) : e;  // exact power of two: x * 2^-e == x / 2^e
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const float q = Elem<T>::ld(v.e[j]) * pinv;
@@ -2089,11 +2291,13 @@ __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__res
                                                                    int64_t nvec, int64_t cv,
                                                                    FastDiv fcv,
                                                                    const float *__restrict__ scale,
-                                                                   int per_row, int round_dtype) {
+                                                                   int per_row, int round_dtype,
+                                                                   int native) {
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    export_fp8_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cv, fcv, scale, per_row, round_dtype);
+    export_fp8_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cv, fcv, scale, per_row, round_dtype,
+                                 native);
 }
 template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__restrict__ x,
@@ -2113,20 +2317,21 @@ __global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__r
                                                                      int64_t nvec, int64_t vpb,
                                                                      FastDiv fvpb,
                                                                      const float *__restrict__ sblk,
-                                                                     const float *__restrict__ s2) {
+                                                                     const float *__restrict__ s2,
+                                                                     int native) {
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    export_nvfp4_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, vpb, fvpb, sblk, s2);
+    export_nvfp4_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, vpb, fvpb, sblk, s2, native);
 }
 template <int U, typename T, int BLOCK>
 __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__restrict__ x,
                                                                      uint8_t *__restrict__ y,
                                                                      uint8_t *__restrict__ sc,
-                                                                     int64_t nvec) {
+                                                                     int64_t nvec, int native) {
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
 #pragma unroll
-  for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK>(base + u * kThreads, x, y, sc, nvec);
+  for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK>(base + u * kThreads, x, y, sc, nvec, native);
 }
 
 int export_u() {
@@ -2147,6 +2352,15 @@ template <class F> void with_export_u(F &&f) {
     f(std::integral_constant<int, 1>{});
   else
     f(std::integral_constant<int, 2>{});
+}
+// MTQ_AMD_EXPORT_NATIVE=0: emulated conversions only (A/B of the native fast paths)
+int export_native() {
+  static int n = -1;
+  if (n < 0) {
+    const char *e = getenv("MTQ_AMD_EXPORT_NATIVE");
+    n = e ? (atoi(e) != 0) : 1;
+  }
+  return n;
 }
 unsigned export_grid(int64_t nvec, int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); }
 
@@ -2552,13 +2766,13 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_fp8_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype);
+            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype, export_native());
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_fp8_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype);
+            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype, export_native());
         });
     } else {
       export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
@@ -2619,13 +2833,13 @@ int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int 
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_nvfp4_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2);
+            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2, export_native());
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_nvfp4_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2);
+            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2, export_native());
         });
     } else {
       export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
@@ -2664,12 +2878,12 @@ int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int 
       if (block == 32)
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
-          export_mxfp4_vec_kernel<U, T, 32><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+          export_mxfp4_vec_kernel<U, T, 32><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, export_native());
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
-          export_mxfp4_vec_kernel<U, T, 16><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec);
+          export_mxfp4_vec_kernel<U, T, 16><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, export_native());
         });
     } else {
       export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(
