@@ -402,6 +402,15 @@ __global__ __launch_bounds__(kThreads) void ew_group_sk_kernel(const T *__restri
   }
 }
 
+int group_u() {
+  static int u = -1;
+  if (u < 0) {
+    const char *e = getenv("MTQ_AMD_GROUP_U");
+    u = e ? atoi(e) : 2;
+  }
+  return u;
+}
+
 int group_variant() {
   static int v = -1;
   if (v < 0) {
@@ -440,15 +449,27 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
       const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
       const bool sk = gv != 3 && op.amax_dtype == MTQ_F32 && op.small && axis_size * vb == nvec;
       if (nvec > 0 && sk) {
-        auto go = [&](auto lc) {
-          constexpr int L = decltype(lc)::value;
-          ew_group_sk_kernel<T, VecOp<T>, U, L><<<g, kThreads, 0, stream>>>(
+        // vectors per lane: U = 2 by default; MTQ_AMD_GROUP_U = 1 or 4 for A/B (LPB = VB / U)
+        auto go = [&](auto uc, auto lc) {
+          constexpr int UU = decltype(uc)::value, L = decltype(lc)::value;
+          const unsigned gg = (unsigned)((nvec + (int64_t)kThreads * UU - 1) / ((int64_t)kThreads * UU));
+          ew_group_sk_kernel<T, VecOp<T>, UU, L><<<gg, kThreads, 0, stream>>>(
               reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
               reinterpret_cast<const float *>(op.amax), axis_size, op);
         };
-        if (vb == 16) go(std::integral_constant<int, 8>{});
-        else if (vb == 32) go(std::integral_constant<int, 16>{});
-        else go(std::integral_constant<int, 32>{});
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I4 = std::integral_constant<int, 4>;
+        const int gu = group_u();
+        if (vb == 16) {
+          if (gu == 1) go(I1{}, std::integral_constant<int, 16>{});
+          else if (gu == 4) go(I4{}, std::integral_constant<int, 4>{});
+          else go(I2{}, std::integral_constant<int, 8>{});
+        } else if (vb == 32) {
+          go(I2{}, std::integral_constant<int, 16>{});
+        } else {
+          go(I2{}, std::integral_constant<int, 32>{});
+        }
       } else if (nvec > 0)
         ew_group_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec, (int)(vb / U), op);
@@ -2042,6 +2063,24 @@ __device__ __forceinline__ float div_rn_pz(float q, float s, float r) {
   return __builtin_fmaf(e, r, y0) + 0.0f;
 }
 
+// div_rn on a pair through the packed fp32 ALU (v_pk_mul_f32 / v_pk_fma_f32: two lanes' worth of
+// work per issue), and the pair's dtype re-rounding (bf16: one v_cvt_pk_bf16_f32).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t div_rn2(f32x2_t q, float s, float r) {
+  const f32x2_t sv = {s, s}, rv = {r, r};
+  const f32x2_t y0 = q * rv;
+  const f32x2_t e = __builtin_elementwise_fma(-y0, sv, q);
+  const f32x2_t y = __builtin_elementwise_fma(e, rv, y0);
+  return (f32x2_t){__builtin_copysignf(y.x, q.x), __builtin_copysignf(y.y, q.y)};
+}
+template <typename T> __device__ __forceinline__ f32x2_t round_pair(f32x2_t d) {
+  if constexpr (std::is_same_v<T, __bf16>) {
+    return __builtin_convertvector(__builtin_convertvector(d, bf16x2_t), f32x2_t);
+  } else {
+    return (f32x2_t){Elem<T>::ld(Elem<T>::st(d.x)), Elem<T>::ld(Elem<T>::st(d.y))};
+  }
+}
+
 template <typename T, bool IDX32>
 __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restrict__ x,
                                                                    uint8_t *__restrict__ y,
@@ -2063,10 +2102,12 @@ __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restric
     float q[N];
     bool inrange = true;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      q[j] = div_rn(Elem<T>::ld(v.e[j]), s, r);
-      if (round_dtype) q[j] = Elem<T>::ld(Elem<T>::st(q[j]));
-      inrange &= fabsf(q[j]) <= kE4M3Max;
+    for (int j = 0; j < N; j += 2) {
+      f32x2_t d = div_rn2((f32x2_t){Elem<T>::ld(v.e[j]), Elem<T>::ld(v.e[j + 1])}, s, r);
+      if (round_dtype) d = round_pair<T>(d);
+      q[j] = d.x;
+      q[j + 1] = d.y;
+      inrange &= (fabsf(d.x) <= kE4M3Max) & (fabsf(d.y) <= kE4M3Max);
     }
     if (inrange) {
       uint32_t w[N / 4];
