@@ -2088,12 +2088,13 @@ __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restric
                                                                    FastDiv fcv,
                                                                    const float *__restrict__ scale,
                                                                    int per_row, int round_dtype,
-                                                                   int native) {
+                                                                   int native, float s_t) {
   using V = Vec<T>;
   constexpr int N = V::N;
   if (i >= nvec) return;
   V v = ldg_vec_nt(x + i * N);
-  const float s = scale[per_row ? idx_div<IDX32>(i, cv, fcv) : 0];
+  // per-tensor: the scalar-loaded s_t (no per-lane load and its latency before the division)
+  const float s = per_row ? scale[idx_div<IDX32>(i, cv, fcv)] : s_t;
   const float r = 1.0f / s;
   uint32_t b[N];
   if (native) {
@@ -2137,6 +2138,23 @@ __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restric
     st_packed_nt(y + i * N, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
 }
 
+// two INT4 codes (rows 2p, 2p+1) of quotients: rint, clamp to [-8, 7], NaN -> 0 (int8 cast)
+__device__ __forceinline__ uint32_t int4_pair(float d0, float d1) {
+  float q0 = __builtin_rintf(d0), q1 = __builtin_rintf(d1);
+  q0 = q0 < -8.f ? -8.f : (q0 > 7.f ? 7.f : q0);
+  q1 = q1 < -8.f ? -8.f : (q1 > 7.f ? 7.f : q1);
+  const int v0 = q0 != q0 ? 0 : (int)q0, v1 = q1 != q1 ? 0 : (int)q1;
+  return ((uint32_t)v0 & 0xFu) | (((uint32_t)v1 & 0xFu) << 4);
+}
+// one INT4 code from a div_rn quotient d of weight x: a NaN d with a non-NaN x is an overflowing
+// or infinite IEEE quotient, i.e. the clamp bound on x's side
+__device__ __forceinline__ uint32_t int4_pair_nan(float d, float x) {
+  float q = __builtin_rintf(d);
+  q = q < -8.f ? -8.f : (q > 7.f ? 7.f : q);
+  const int v = q == q ? (int)q : (x != x ? 0 : (x < 0.f ? -8 : 7));
+  return (uint32_t)v & 0xFu;
+}
+
 // rows (2p, 2p+1) x N columns -> N bytes
 template <typename T, bool IDX32>
 __device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restrict__ x,
@@ -2155,28 +2173,23 @@ __device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restri
   const int64_t cb = idx_div<IDX32>(c0, block, fblk);
   const float s0 = scale[(2 * pr) * nblk + cb], s1 = scale[(2 * pr + 1) * nblk + cb];
   const float r0 = 1.0f / s0, r1 = 1.0f / s1;
-  // div_rn is the IEEE quotient except where that quotient overflows or the operands are not
-  // finite / positive (div_rn then gives NaN, IEEE +-inf): a lane that saw a NaN quotient (rare;
-  // NaN weights included, which give the same bytes either way) repacks its vector with the IEEE
-  // division operator.
+  // div_rn is the IEEE quotient except where that quotient overflows or is infinite (div_rn
+  // gives NaN there, IEEE +-inf -> the clamp's -8 / 7, selected from the weight's sign) and where
+  // 1/s is not finite (a zero, subnormal or non-finite scale: that lane, rare and uniform over its
+  // vector, repacks with the IEEE division operator).
   uint32_t b[N];
-  bool redo = false;
-  auto pack = [&](auto ieee) {
+  constexpr float kInf = __builtin_huge_valf();
+  if (__builtin_expect(r0 < kInf && r1 < kInf && s0 < kInf && s1 < kInf, 1)) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const float x0 = Elem<T>::ld(lo.e[j]), x1 = Elem<T>::ld(hi.e[j]);
-      const float d0 = decltype(ieee)::value ? x0 / s0 : div_rn(x0, s0, r0);
-      const float d1 = decltype(ieee)::value ? x1 / s1 : div_rn(x1, s1, r1);
-      if (!decltype(ieee)::value) redo |= (d0 != d0) | (d1 != d1);
-      float q0 = __builtin_rintf(d0), q1 = __builtin_rintf(d1);
-      q0 = q0 < -8.f ? -8.f : (q0 > 7.f ? 7.f : q0);
-      q1 = q1 < -8.f ? -8.f : (q1 > 7.f ? 7.f : q1);
-      const int v0 = q0 != q0 ? 0 : (int)q0, v1 = q1 != q1 ? 0 : (int)q1;
-      b[j] = ((uint32_t)v0 & 0xFu) | (((uint32_t)v1 & 0xFu) << 4);
+      b[j] = int4_pair_nan(div_rn(x0, s0, r0), x0) | (int4_pair_nan(div_rn(x1, s1, r1), x1) << 4);
     }
-  };
-  pack(std::false_type{});
-  if (redo) pack(std::true_type{});
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      b[j] = int4_pair(Elem<T>::ld(lo.e[j]) / s0, Elem<T>::ld(hi.e[j]) / s1);
+  }
   if constexpr (N == 8)
     st_packed_nt(y + pr * cols + c0, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
                  b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
@@ -2334,11 +2347,12 @@ __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__res
                                                                    const float *__restrict__ scale,
                                                                    int per_row, int round_dtype,
                                                                    int native) {
+  const float s_t = per_row ? 0.f : scale[0];
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
 #pragma unroll
   for (int u = 0; u < U; ++u)
     export_fp8_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cv, fcv, scale, per_row, round_dtype,
-                                 native);
+                                 native, s_t);
 }
 template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__restrict__ x,
