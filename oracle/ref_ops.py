@@ -226,7 +226,11 @@ def compute_amax_entropy(calib_hist, calib_bin_edges, num_bits, unsigned, stride
 
 
 def compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128):
-    """Restates _compute_amax_mse, calib/histogram.py:285-325 (CPU)."""
+    """Restates _compute_amax_mse, calib/histogram.py:285-325 (CPU), with its call as it binds:
+    ``fake_tensor_quant(centers, amax, num_bits, unsigned)`` puts ``num_bits`` in the ``bias`` slot
+    and ``unsigned`` in ``num_bits`` (FakeTensorQuantFunction.forward, tensor_quant.py:350-394:
+    ``_tensor_quant(centers - bias, amax, unsigned, False, True) + bias``), and
+    ``scaled_e4m3(centers, amax, 4, 3)`` misses ``M`` (TypeError)."""
     counts = torch.from_numpy(calib_hist[:]).float()
     edges = torch.from_numpy(calib_bin_edges[:]).float()
     centers = (edges[1:] + edges[:-1]) / 2
@@ -234,9 +238,9 @@ def compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, 
     for i in range(start_bin, len(centers), stride):
         amax = centers[i]
         if isinstance(num_bits, int) and num_bits >= 0:
-            quant_centers = tensor_quant(centers, amax, num_bits, unsigned)
+            quant_centers = tensor_quant(centers - num_bits, amax, int(unsigned), False, True) + num_bits
         elif num_bits == (4, 3):
-            quant_centers = fp8_eager(centers, amax)
+            raise TypeError("ScaledE4M3Function.forward() missing 1 required positional argument: 'M'")
         else:
             raise TypeError("Invalid num_bits.")
         mse = ((quant_centers - centers) ** 2 * counts).mean()

@@ -4,14 +4,28 @@ Reference: modelopt/torch/quantization/calib/histogram.py:35-343.  ``collect`` k
 reference's torch-histogram branch semantics exactly (``torch.histc(|x|, bins, 0, max)`` with the
 first-call ``linspace`` edges and the fixed-width bin growth of :108-130); the histogram itself is
 one launch of ``histogram_abs_accumulate`` plus one of the max|x| reduction (the reference: abs,
-float copy, max, histc -- and a ``torch.min(x) < 0`` host sync).  Counts are exact integers per
-call (the reference accumulates float counts, which stop at 2^24 per bin).
-``compute_amax`` runs on the host like the reference (entropy / MSE / percentile); the MSE sweep
-quantises the bin centres with the HIP kernels.
+float copy, max, histc -- and a ``torch.min(x) < 0`` host sync).
+
+Counts follow ``torch.histc``'s float semantics (``_histc_counts``): the reference's CPU histc
+splits the (flattened, after ``skip_zeros``) input into one contiguous chunk per intra-op thread,
+counts each chunk into a thread-local fp32 histogram -- a count stops at 2^24, where ``+1`` rounds
+back to 2^24 -- and adds the per-thread histograms in thread order in fp32 (measured on torch
+2.10: chunk counts (2^24+, 3, 3) give 16777224, (3, 3, 2^24+) give 16777222).  The kernel counts
+exact integers per chunk; when a call can hold more than 2^24 elements, the chunks are counted
+separately and folded exactly so, with ``torch.get_num_threads()`` threads (the reference's own
+process setting; ``MTQ_AMD_HIST_THREADS`` overrides).  ``MTQ_AMD_HIST_COUNTS=exact`` keeps exact
+integer counts instead.
+
+``compute_amax`` runs on the host like the reference (entropy / MSE / percentile).  The MSE sweep
+reproduces the reference's actual call ``fake_tensor_quant(centers, amax, num_bits, unsigned)``,
+which binds ``num_bits`` to the functional's ``bias`` slot and ``unsigned`` to ``num_bits``
+(histogram.py:305-312 vs tensor_quant.py:349-391); ``MTQ_AMD_HIST_MSE=intent`` quantises with the
+documented intent instead (``num_bits``-bit, no bias).
 """
 
 from __future__ import annotations
 
+import os
 import warnings
 from collections import Counter
 
@@ -75,9 +89,7 @@ class HistogramCalibrator(_Calibrator):
             bins = self._num_bins
             hmax = self._calib_bin_edges[-1].to(device=x.device, dtype=torch.float32).reshape(())
             old = self._calib_hist
-        counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
-        _ops().histogram_abs_accumulate(x, hmax.float().contiguous(), counts, bins, self._skip_zeros)
-        hist = counts.float()
+        hist = _histc_counts(x, hmax.float().contiguous(), bins, self._skip_zeros)
         if old is not None:
             hist[: old.numel()] += old.to(hist.device)
         self._calib_hist = hist
@@ -118,6 +130,59 @@ class HistogramCalibrator(_Calibrator):
         else:
             e = f"[{float(self._calib_bin_edges[0]):.3f}, ..., {float(self._calib_bin_edges[-1]):.3f}]({len(self._calib_bin_edges)})"
         return f"HistogramCalibrator(calib_bin_edges={e})"
+
+
+_HISTC_GRAIN = 32768  # at::internal::GRAIN_SIZE: the parallel_for grain of the CPU histc
+_F32_COUNT_LIMIT = 2**24  # an fp32 counter stops here: 2^24 + 1 rounds to 2^24 (ties to even)
+
+
+def _histc_threads() -> int:
+    env = os.environ.get("MTQ_AMD_HIST_THREADS")
+    return max(1, int(env)) if env else max(1, torch.get_num_threads())
+
+
+def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bool) -> torch.Tensor:
+    """fp32 per-call histogram of |x| over [0, hmax] with torch.histc's CPU accumulation.
+
+    Every count of a call with at most 2^24 (kept) elements is exact in fp32 whatever the chunking,
+    so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T`` threads,
+    chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted by its own launch (exact
+    integers), clamped at 2^24 and added into the fp32 result in thread order."""
+    ops = _ops()
+    n = x.numel()
+    mode = os.environ.get("MTQ_AMD_HIST_COUNTS", "histc")
+    if n <= _F32_COUNT_LIMIT or mode == "exact":
+        counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
+        ops.histogram_abs_accumulate(x, hmax, counts, bins, skip_zeros)
+        return counts.float()
+    flat = x.contiguous().reshape(-1)
+    if skip_zeros:
+        # chunk boundaries live in the compacted (non-zero) index space: map them back
+        csum = torch.cumsum((flat != 0).to(torch.int64), 0)
+        kept = int(csum[-1])
+    else:
+        csum, kept = None, n
+    if kept <= _F32_COUNT_LIMIT:
+        counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
+        ops.histogram_abs_accumulate(flat, hmax, counts, bins, skip_zeros)
+        return counts.float()
+    threads = min(_histc_threads(), -(-kept // _HISTC_GRAIN))
+    chunk = -(-kept // threads)
+    starts = [t * chunk for t in range(threads) if t * chunk < kept] + [kept]
+    if csum is not None:
+        # the first original index whose non-zero rank reaches each compacted start
+        cuts = torch.searchsorted(csum, torch.tensor(starts[1:-1], device=csum.device, dtype=torch.int64) + 1)
+        bounds = [0] + cuts.tolist() + [n]
+    else:
+        bounds = starts
+    hist = torch.zeros(bins, dtype=torch.float32, device=x.device)
+    counts = torch.empty(bins, dtype=torch.int32, device=x.device)
+    for b, e in zip(bounds[:-1], bounds[1:]):
+        counts.zero_()
+        if e > b:
+            ops.histogram_abs_accumulate(flat[b:e], hmax, counts, bins, skip_zeros)
+        hist += counts.float().clamp_(max=_F32_COUNT_LIMIT)
+    return hist
 
 
 def _compute_amax_entropy(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128):
@@ -167,22 +232,46 @@ def _compute_amax_entropy(calib_hist, calib_bin_edges, num_bits, unsigned, strid
     return torch.tensor(calib_bin_edges[last_argmin * stride + start_bin].item())
 
 
+def _reference_call_qdq(centers: torch.Tensor, amax: torch.Tensor, bias: int, num_bits: int) -> torch.Tensor:
+    """What the reference's ``fake_tensor_quant(centers, amax, num_bits, unsigned)`` computes on
+    the CPU (histogram.py:308): ``bias = num_bits`` and ``num_bits = unsigned`` (0 or 1), so
+    FakeTensorQuantFunction.forward (tensor_quant.py:350-394) quantises ``centers - bias`` with
+    ``_tensor_quant(..., num_bits, unsigned=False, narrow_range=True)`` (:607-645) and adds the
+    bias back -- the same fp32 operations, elementwise, in the same order."""
+    x = (centers - bias).float()
+    a = amax.float()
+    max_bound = torch.tensor(2.0 ** (num_bits - 1) - 1.0, dtype=torch.float32)
+    min_bound = -max_bound
+    scale = max_bound / a
+    tiny = bool(a <= 1.0 / (1 << 24))
+    if tiny:
+        scale = torch.zeros_like(scale)
+    out = torch.clamp((x * scale).round_(), min_bound, max_bound)
+    if tiny:
+        scale = torch.ones_like(scale)
+    return (out / scale) + bias
+
+
 def _compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128,
                       device=None):
-    """MSE amax (histogram.py:285-325): every candidate quantises the bin centres on the GPU; the
-    per-candidate MSEs are gathered once instead of one host sync per candidate.
+    """MSE amax (histogram.py:285-325).
 
-    Divergence: the reference calls ``fake_tensor_quant(centers, amax, num_bits, unsigned)``, which
-    binds ``num_bits`` to the functional's ``bias`` slot (tensor_quant.py:337-349), and
-    ``scaled_e4m3(centers, amax, 4, 3)`` (missing M).  Here the candidates are quantised with the
-    documented intent (``num_bits``-bit, narrow range, no bias); MSE amax parity is therefore
-    against that intent, not against the reference's outputs.
+    Default: the reference's actual numbers.  Its call ``fake_tensor_quant(centers, amax, num_bits,
+    unsigned)`` binds ``num_bits`` to ``bias`` (``_reference_call_qdq``), and ``scaled_e4m3(centers,
+    amax, 4, 3)`` lacks ``M`` and raises TypeError -- both reproduced.  The sweep runs on the host
+    in fp32 with the reference's per-candidate op sequence (2048 bins, once per quantizer), so the
+    chosen amax is the reference run's bit for bit (``tests/golden/calib_ref.*``); the reference
+    itself moves it to the GPU when one is present, where its CUDA extension evaluates the
+    0-bit shift of the same call differently (tensor_quant_gpu.cu:38-41) -- parity is pinned to
+    the CPU run.  ``MTQ_AMD_HIST_MSE=intent``: quantise with ``num_bits`` bits (narrow range) and
+    FP8 E4M3 as the code evidently intends, on the calibrator's device with the HIP kernels.
     """
     if calib_bin_edges is None and calib_hist is None:
         return None
+    intent = os.environ.get("MTQ_AMD_HIST_MSE", "reference") == "intent"
     counts = torch.from_numpy(calib_hist[:]).float()
     edges = torch.from_numpy(calib_bin_edges[:]).float()
-    if device is not None and device.type == "cuda":
+    if intent and device is not None and device.type == "cuda":
         counts = counts.to(device)
         edges = edges.to(device)
     centers = (edges[1:] + edges[:-1]) / 2
@@ -190,8 +279,13 @@ def _compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1,
     for i in range(start_bin, len(centers), stride):
         amax = centers[i]
         if isinstance(num_bits, int) and num_bits >= 0:
-            quant_centers = fake_tensor_quant(centers, amax, None, num_bits, unsigned)
+            if intent:
+                quant_centers = fake_tensor_quant(centers, amax, None, num_bits, unsigned)
+            else:
+                quant_centers = _reference_call_qdq(centers, amax, num_bits, int(unsigned))
         elif num_bits == (4, 3):
+            if not intent:
+                raise TypeError("ScaledE4M3Function.forward() missing 1 required positional argument: 'M'")
             quant_centers = fp8_fake_quant(centers, amax)
         else:
             raise TypeError("Invalid num_bits. num_bits must be a positive integer or tuple (4,3).")
@@ -199,7 +293,10 @@ def _compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1,
         arguments.append(i)
     mses_np = torch.stack(mses).cpu().numpy()
     argmin = np.argmin(mses_np)
-    return centers[arguments[argmin]]
+    calib_amax = centers[arguments[argmin]]
+    if device is not None:
+        calib_amax = calib_amax.to(device)
+    return calib_amax
 
 
 def _compute_amax_percentile(calib_hist, calib_bin_edges, percentile):

@@ -16,6 +16,7 @@ from __future__ import annotations
 import math
 import os
 import warnings
+import weakref
 from collections.abc import Callable
 
 import torch
@@ -24,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from modelopt_amd._ext import ops as _ops
-from modelopt_amd.torch.utils.distributed import DistributedProcessGroup, fixed_order_sum
+from modelopt_amd.torch.utils.distributed import DistributedProcessGroup, fixed_order_sum_many
 
 from .conversion import set_quantizer_by_cfg_context
 from .nn.modules.quant_module import QuantModule
@@ -273,8 +274,10 @@ def get_scale(x_max, w_max, alpha, tensor_parallel_group=None):
 
 class _AWQLiteHelper:
     cache_mode: bool = False
+    _live: "weakref.WeakSet[_AWQLiteHelper]" = weakref.WeakSet()
 
     def __init__(self, module, name, alpha_step):
+        _AWQLiteHelper._live.add(self)
         self.name = name
         self.act_scale = 0.0
         self.num_cache_steps = 0
@@ -347,6 +350,7 @@ def _mse_fast(out, ref) -> bool:
 # wider linears keep hipBLASLt for the GEMM (its 1.5 PFLOP/s vs the fused kernel's ~1.0).
 # MTQ_AMD_AWQ_FUSED: "auto" (default), "always", "never".
 _AWQ_FUSED_MAX_N = 2048
+_AWQ_FUSED_MAX_G = 64
 _AWQ_FUSED = os.environ.get("MTQ_AMD_AWQ_FUSED", "auto")
 # Budget for keeping every alpha's quantised weight [11, N, K] across the search batches (it does
 # not change between batches; the reference recomputes it per batch): a fraction of the HBM free
@@ -397,18 +401,29 @@ def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
     ops = _ops()
     bias = self.bias.detach() if self.bias is not None else None
     x2 = input.reshape(-1, input.shape[-1])
-    fused = _AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and w.shape[0] <= _AWQ_FUSED_MAX_N)
+    n_out, k_in, n_alpha = w.shape[0], w.shape[1], len(helper.alphas)
+    # the fused kernel's limits (mtq_awq_search_gemm: G <= 64, 32-bit element offsets); the
+    # batched path's loss pass takes G <= 16; anything else runs one alpha at a time
+    fused_ok = n_alpha <= _AWQ_FUSED_MAX_G and x2.shape[0] * k_in < 2**31 and n_out * k_in < 2**31
+    fused = fused_ok and (_AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and n_out <= _AWQ_FUSED_MAX_N))
     if fused:
         ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
-    elif len(helper.alphas) <= 16:
+    elif n_alpha <= 16:
         # wide linears: x * (1/s) for every alpha in one pass, the alphas' GEMMs as one batched
         # hipBLASLt call (bias in its fp32 epilogue, one rounding, as F.linear), all losses in
         # one pass that reads out_actual once
         # (per-alpha torch.mm into slices of one [G, M, N] output, the GEMM F.linear itself uses:
         # torch.bmm with the transposed [G, K, N] weight view faulted the GPU in hipBLASLt on
         # ROCm 7 at [11, 8192, 4096] x [11, 4096, 4096])
-        xs = ops.awq_prescale(x2, sinv)
-        out = torch.empty((xs.shape[0], xs.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+        try:
+            xs = ops.awq_prescale(x2, sinv)
+            out = torch.empty((xs.shape[0], xs.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+        except torch.cuda.OutOfMemoryError:
+            # the cached [G, N, K] weights of the other linears hold the HBM: drop them, retry
+            xs = None
+            _awq_release_wq_caches()
+            xs = ops.awq_prescale(x2, sinv)
+            out = torch.empty((xs.shape[0], xs.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
         for ai in range(xs.shape[0]):
             if bias is None:
                 torch.mm(xs[ai], wq[ai].t(), out=out[ai])
@@ -487,8 +502,13 @@ def _awq_forward(self, input, *args, **kwargs):
 
 
 @torch.no_grad()
-def apply_pre_quant_scale_and_smooth(linear: nn.Module, pre_quant_scale: torch.Tensor | None = None):
-    """Fold 1/pre_quant_scale into the weight and re-calibrate it (reference :1209-1270)."""
+def apply_pre_quant_scale_and_smooth(linear: nn.Module, pre_quant_scale: torch.Tensor | None = None,
+                                     _distributed_sync: bool = True):
+    """Fold 1/pre_quant_scale into the weight and re-calibrate it (reference :1209-1270).
+
+    ``_distributed_sync=False`` (awq_lite): the folded weights are bit-identical on every DP rank
+    by construction (act_scale and losses are synced before the choice), so the reference's
+    per-linear weight-amax all_reduce(MAX) is an identity and is skipped."""
     assert is_quantized_linear(linear), "Only quantized linear modules are supported"
     assert linear.input_quantizer.pre_quant_scale is None, "pre_quant_scale should be None first!"
     if pre_quant_scale is None:
@@ -504,12 +524,134 @@ def apply_pre_quant_scale_and_smooth(linear: nn.Module, pre_quant_scale: torch.T
         (linear.weight * inv_scale.to(linear.weight.device).squeeze()[None, :]).to(linear.weight.dtype)
     )
     linear.weight_quantizer.reset_amax()
-    max_calibrate(linear, lambda lin: lin.weight_quantizer(lin.weight))
+    max_calibrate(linear, lambda lin: lin.weight_quantizer(lin.weight), distributed_sync=_distributed_sync)
     if linear.input_quantizer.amax is not None:
         assert hasattr(linear.input_quantizer, "_amax_for_smoothing")
         dev, dt = linear.weight.device, linear.weight.dtype
         a = linear.input_quantizer._amax_for_smoothing.to(device=dev, dtype=dt)
         linear.input_quantizer.amax = (a * pre_quant_scale.to(dev)).amax().to(dt)
+
+
+def _awq_dp_groups(awq_modules):
+    """The AWQ linears grouped by their initialised data-parallel group, in module order (the
+    same on every rank); linears without one are returned under key None."""
+    groups: dict = {}
+    for name, module in awq_modules:
+        g = module.parallel_state.data_parallel_group if module.parallel_state is not None else None
+        key = None if g is None or not g.is_initialized() else (id(g.group) if g.group is not None else 0)
+        groups.setdefault(key, (g, []))[1].append((name, module))
+    return groups
+
+
+def _awq_sync_act_scale(awq_modules):
+    """After the caching pass: act_scale = mean over the cache steps, NaN check, DP average.
+
+    Reference :1595-1629 issues, per linear, an ``all_gather_object`` of a NaN flag and an
+    ``all_reduce(AVG)`` of act_scale, both gated on the rank-local ``num_cache_steps > 0`` (a
+    linear that saw tokens on one rank only -- an MoE expert -- would enter the collectives on
+    that rank alone).  Here every linear of a DP group contributes ``[act_scale, nan, present]``
+    (zeros when it saw no tokens) to ONE fixed-order sum (``fixed_order_sum_many``: one all_gather
+    per group, independent of the number of linears), and every rank takes the same decision:
+    disabled when a rank saw NaN or no rank saw tokens, otherwise act_scale = sum of the ranks that
+    saw tokens / their count (the reference's AVG when all ranks saw tokens), rounded back to the
+    act_scale dtype."""
+    for key, (g, mods) in _awq_dp_groups(awq_modules).items():
+        if key is None:
+            for _, module in mods:
+                h = module.awq_lite
+                if h.num_cache_steps == 0:
+                    h.is_enabled = False
+                    continue
+                module._if_calib = True
+                h.act_scale = h.act_scale / h.num_cache_steps
+                if bool(torch.isnan(h.act_scale).any() or torch.isnan(h.weight_scale).any()):
+                    h.is_enabled = False
+            continue
+        parts = []
+        for _, module in mods:
+            h = module.awq_lite
+            k = module.weight.shape[1]
+            dev = h.weight_scale.device
+            if h.num_cache_steps > 0:
+                a = (h.act_scale / h.num_cache_steps).reshape(-1)
+                nan = (torch.isnan(a).any() | torch.isnan(h.weight_scale).any()).reshape(1)
+                present = torch.ones(1, device=dev)
+            else:
+                a = torch.zeros(k, device=dev)
+                nan = torch.zeros(1, device=dev)
+                present = torch.zeros(1, device=dev)
+            parts += [a.to(device=dev, dtype=torch.float32), nan.to(torch.float32), present]
+        summed = fixed_order_sum_many(parts, g)
+        for i, (_, module) in enumerate(mods):
+            h = module.awq_lite
+            a, nan, present = summed[3 * i : 3 * i + 3]
+            n_present, n_nan = float(present), float(nan)  # host reads of one gathered buffer
+            if n_present == 0 or n_nan > 0:
+                h.is_enabled = False
+                continue
+            module._if_calib = True
+            dtype = h.act_scale.dtype if isinstance(h.act_scale, torch.Tensor) else torch.float32
+            h.act_scale = (a / n_present).to(dtype)
+            h.dp_group = g
+            h._dp_cache_steps = n_present
+
+
+def _awq_sync_losses(awq_modules):
+    """After the search pass: per-alpha losses summed over the DP ranks in rank order (one
+    collective per group), and the reference's "search pass missed this linear" check
+    (:1661-1671) taken on the group-wide counts so every rank disables the same linears.
+
+    Divergence from the reference (which keeps each rank's local losses, so ranks with different
+    data can pick different alphas and end with different weights): every rank picks the alpha a
+    single process over all the data would."""
+    for key, (g, mods) in _awq_dp_groups(awq_modules).items():
+        if key is None:
+            searched = {name: module.awq_lite.num_search_steps > 0 for name, module in mods}
+            cached = {name: module.awq_lite.num_cache_steps > 0 for name, module in mods}
+        else:
+            parts = []
+            for _, module in mods:
+                h = module.awq_lite
+                dev = h.loss.device
+                parts += [h.loss, torch.full((1,), float(h.num_search_steps > 0), device=dev),
+                          torch.full((1,), float(h.num_cache_steps > 0), device=dev)]
+            summed = fixed_order_sum_many(parts, g)
+            searched, cached = {}, {}
+            for i, (name, module) in enumerate(mods):
+                h = module.awq_lite
+                loss, s, c = summed[3 * i : 3 * i + 3]
+                h.loss = loss.to(h.loss.device)
+                searched[name], cached[name] = float(s) > 0, float(c) > 0
+        for name, module in mods:
+            h = module.awq_lite
+            if cached[name] and not searched[name] and h.is_enabled:
+                h.is_enabled = False
+                warnings.warn(
+                    f"awq_lite: Calling `forward_loop(model)` the second time did not forward data through the {name}."
+                )
+
+
+def _awq_wq_cache_budget() -> int:
+    """HBM for the [G, N, K] quantised-weight cache of the search: a fraction of the free HBM,
+    divided among the processes that share this device (ranks of one node on fewer GPUs: the
+    2-rank tests and the C4 pipeline rehearsal on one MI355X), each of which would otherwise claim
+    the same free memory."""
+    free = torch.cuda.mem_get_info()[0]
+    local = os.environ.get("LOCAL_WORLD_SIZE")
+    if local:
+        local = int(local)
+    else:  # spawned workers without torchrun's env: one node assumed
+        local = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    per_dev = max(1, -(-local // max(1, torch.cuda.device_count())))
+    return int(free * _AWQ_WQ_CACHE_FRACTION / per_dev)
+
+
+def _awq_release_wq_caches():
+    """Drop every cached [G, N, K] search weight (after an allocation failure in the search)."""
+    for h in list(_AWQLiteHelper._live):
+        h._wq_all = None
+    _awq_wq_budget[0] = 0  # no new caching after a failure
+    torch.cuda.empty_cache()
 
 
 @torch.no_grad()
@@ -530,29 +672,16 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
         max_calibrate(model, lambda m: None, distributed_sync=True)
     finish_stats_collection(model)
 
-    for _, module in model.named_modules():
-        if is_quantized_linear(module) and hasattr(module, "awq_lite") and module.awq_lite.num_cache_steps > 0:
-            module._if_calib = True
-            h = module.awq_lite
-            h.act_scale = h.act_scale / h.num_cache_steps
-            has_nan_local = bool(torch.isnan(h.act_scale).any() or torch.isnan(h.weight_scale).any())
-            g = module.parallel_state.data_parallel_group
-            has_nan = DistributedProcessGroup.get_dist_syncd_obj(has_nan_local, g, lambda objs: any(objs))
-            if has_nan:
-                h.is_enabled = False
-            elif g.is_initialized():
-                # reference :1588-1593 all_reduce(AVG): here a fixed-order fp32 sum / world, so
-                # every rank and every run gets the same bits (and gloo, which lacks AVG, works)
-                h.act_scale = fixed_order_sum(h.act_scale, g) / g.world_size()
-                h.dp_group = g
-    for _, module in model.named_modules():
-        if is_quantized_linear(module) and hasattr(module, "awq_lite") and module.awq_lite.num_cache_steps == 0:
-            module.awq_lite.is_enabled = False
+    awq_modules = [
+        (name, module) for name, module in model.named_modules()
+        if is_quantized_linear(module) and isinstance(getattr(module, "awq_lite", None), _AWQLiteHelper)
+    ]
+    _awq_sync_act_scale(awq_modules)
 
     _AWQLiteHelper.cache_mode = False
     if torch.cuda.is_available():
         torch.cuda.empty_cache()
-        _awq_wq_budget[0] = int(torch.cuda.mem_get_info()[0] * _AWQ_WQ_CACHE_FRACTION)
+        _awq_wq_budget[0] = _awq_wq_cache_budget()
     forward_loop(model)
     _awq_wq_budget[0] = 0
     for _, module in model.named_modules():
@@ -560,19 +689,15 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
         if isinstance(h, _AWQLiteHelper):
             h._wq_all = None
             h._tables = None
+    _awq_sync_losses(awq_modules)
 
     def postprocess(module, name):
         h = module.awq_lite
         if h.is_enabled:
-            if h.dp_group is not None:
-                # Divergence from the reference (which keeps each rank's local losses, so ranks with
-                # different data can pick different alphas and end with different weights): the
-                # per-alpha losses are summed over the DP ranks in rank order, so every rank picks
-                # the alpha a single process over all the data would.
-                h.loss = fixed_order_sum(h.loss, h.dp_group)
             losses = h.loss.tolist()  # one host read per layer
-            loss = dict(zip(h.alphas, losses))
-            h.best_alpha = min(loss, key=loss.get)
+            # the reference's loss dict of floats (update_best_params, :1497-1511)
+            h.loss = dict(zip(h.alphas, losses))
+            h.best_alpha = min(h.loss, key=h.loss.get)
             h.best_scale = get_scale(h.act_scale, h.weight_scale, h.best_alpha, None)
         for q in (module.weight_quantizer, module.input_quantizer):
             if hasattr(q, "_pre_quant_scale"):
@@ -586,23 +711,18 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
                 module.input_quantizer.amax = act_amax.amax()
             module.input_quantizer.enable()
         if h.is_enabled:
-            apply_pre_quant_scale_and_smooth(module, 1.0 / h.best_scale)
+            apply_pre_quant_scale_and_smooth(module, 1.0 / h.best_scale, _distributed_sync=False)
         else:
             warnings.warn(f"awq_lite: Disabling for {name}, quantizing with max calibration.")
-            max_calibrate(module, lambda m: m.weight_quantizer(m.weight))
+            max_calibrate(module, lambda m: m.weight_quantizer(m.weight), distributed_sync=False)
 
     for name, module in model.named_modules():
         if not hasattr(module, "awq_lite"):
             continue
         h = module.awq_lite
-        if h.num_cache_steps > 0 and h.num_search_steps == 0:
-            h.is_enabled = False
-            warnings.warn(
-                f"awq_lite: Calling `forward_loop(model)` the second time did not forward data through the {name}."
-            )
         if not h.is_enabled:
             warnings.warn(f"awq_lite: Forcing pre_quant_scale=1 for {name}.")
-            max_calibrate(module, lambda m: m.weight_quantizer(m.weight))
+            max_calibrate(module, lambda m: m.weight_quantizer(m.weight), distributed_sync=False)
             module.input_quantizer._enable_pre_quant_scale = True
             module.input_quantizer.pre_quant_scale = torch.ones(
                 module.weight.shape[1], dtype=module.weight.dtype, device=module.weight.device

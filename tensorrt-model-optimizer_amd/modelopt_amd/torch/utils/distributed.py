@@ -84,6 +84,24 @@ def fixed_order_sum(t: torch.Tensor, group: DistributedProcessGroup) -> torch.Te
     return acc.to(dev)
 
 
+def fixed_order_sum_many(tensors: list[torch.Tensor], group: DistributedProcessGroup) -> list[torch.Tensor]:
+    """``fixed_order_sum`` of many tensors with ONE collective: all are flattened into one fp32
+    buffer (every rank must pass the same shapes in the same order), gathered once, summed in
+    rank order and split back (fp32, on the first tensor's device).  AWQ-lite uses it for the
+    act_scale / NaN flags of every linear after the caching pass and for every linear's losses
+    after the search pass: two collectives per calibration instead of two or three per linear."""
+    if not tensors:
+        return []
+    flat = torch.cat([t.detach().reshape(-1).to(device=tensors[0].device, dtype=torch.float32) for t in tensors])
+    summed = fixed_order_sum(flat, group) if group.is_initialized() else flat
+    out, off = [], 0
+    for t in tensors:
+        n = t.numel()
+        out.append(summed[off : off + n].reshape(t.shape))
+        off += n
+    return out
+
+
 class ParallelState:
     """Data / tensor / expert parallel groups of a module (reference :441-466)."""
 

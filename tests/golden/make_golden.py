@@ -15,9 +15,11 @@ Outputs (small; committed):
   tensor_quant.safetensors   INT `_tensor_quant`, FP8 `fp8_eager`, `reduce_amax` cases
   quantizer.safetensors      TensorQuantizer calibrate+quant cases (per-tensor, axis, block, padding)
   calib.safetensors/.json    MaxCalibrator / HistogramCalibrator (+ entropy / percentile amax)
+  calib_ref.safetensors/.json HistogramCalibrator at > 2^24 counts per call (1 / 3 threads) + MSE amax
   mtq_linear.safetensors     C1: mtq.quantize(nn.Linear(1024,1024), INT8_DEFAULT_CFG)
   llama_fp8.safetensors      C2 class: tiny LlamaForCausalLM FP8_DEFAULT_CFG PTQ (amax + logits)
   awq.safetensors/.json      C3 class: awq_lite on a small MLP (best alpha/scale, weights, amax)
+  awq_b128.safetensors/.json C3 proper: INT4_AWQ_CFG (block 128) in bf16 on K % 128 == 0 linears
   presets.json               the reference preset configs
   mx_kat.json                the MX known-answer tables of test_quantize_mxformats_cuda.py (data)
 """
@@ -217,6 +219,55 @@ def gen_calib():
     (OUT / "calib.json").write_text(json.dumps(meta, indent=1))
 
 
+def gen_calib_ref():
+    """HistogramCalibrator at its real semantics (calib/histogram.py:77-130, 285-325):
+    * torch.histc's fp32 counts on 40 M-element peaked tensors (one bin > 2^24 per call), with 1
+      and 3 intra-op threads (the per-thread fp32 saturation and the thread-order fold), a second
+      call that grows the bins, and a skip_zeros case;
+    * entropy / percentile / MSE amax from those histograms;
+    * MSE amax for int 8 signed / unsigned and int 4 on the small ``calib`` batches -- the
+      reference's ``fake_tensor_quant(centers, amax, num_bits, unsigned)`` call as it runs -- and
+      the TypeError of the (4, 3) branch."""
+    sys.path.insert(0, str(OUT))
+    from hist_inputs import peaked
+
+    t, meta = {}, {"cases": []}
+    nthreads = torch.get_num_threads()
+    for threads, skip in [(1, False), (3, False), (3, True)]:
+        torch.set_num_threads(threads)
+        h = HistogramCalibrator(8, None, False, num_bins=2048, skip_zeros=skip)
+        for scale in (1.0, 1.5):
+            h.collect(peaked(scale=scale, zeros_every=4 if skip else 0))
+        key = f"t{threads}_skip{int(skip)}"
+        t[f"hist_{key}"] = h._calib_hist.clone()
+        t[f"edges_{key}"] = h._calib_bin_edges.clone()
+        case = {"key": key, "threads": threads, "skip_zeros": skip, "num_bins": h._num_bins,
+                "max_count": float(h._calib_hist.max())}
+        case["percentile_9999"] = float(h.compute_amax("percentile", percentile=99.99))
+        case["mse"] = float(h.compute_amax("mse"))
+        if threads == 3 and not skip:
+            case["entropy"] = float(h.compute_amax("entropy"))
+        meta["cases"].append(case)
+    torch.set_num_threads(nthreads)
+    # MSE method on the small calib batches (int 8 / unsigned / int 4), FP8 raises
+    g = torch.Generator().manual_seed(20)
+    xs = [torch.randn(32, 64, generator=g) * s for s in (1.0, 2.5, 0.7)]
+    for nb, u in [(8, False), (8, True), (4, False)]:
+        h = HistogramCalibrator(nb, None, u, num_bins=256)
+        for x in xs:
+            h.collect(x.abs() if u else x)
+        meta[f"small_mse_b{nb}_u{int(u)}"] = float(h.compute_amax("mse", start_bin=16))
+    h = HistogramCalibrator((4, 3), None, False, num_bins=256)
+    h.collect(xs[0])
+    try:
+        h.compute_amax("mse", start_bin=16)
+        meta["fp8_mse_error"] = None
+    except TypeError as e:
+        meta["fp8_mse_error"] = "TypeError: " + str(e)
+    save_file(t, str(OUT / "calib_ref.safetensors"))
+    (OUT / "calib_ref.json").write_text(json.dumps(meta, indent=1))
+
+
 def gen_mtq_linear():
     torch.manual_seed(30)
     m = nn.Linear(1024, 1024)
@@ -354,6 +405,71 @@ def gen_awq():
     t["out"] = model(test).detach()
     save_file(t, str(OUT / "awq.safetensors"))
     (OUT / "awq.json").write_text(json.dumps(meta, indent=1))
+
+
+class _WideMLP(nn.Module):
+    """K % 128 == 0 everywhere; output widths on both sides of the fused-search crossover
+    (N = 2304 above it; 256 and 1024 at or below it), one linear without bias."""
+
+    def __init__(self):
+        super().__init__()
+        self.net = nn.Sequential(
+            nn.Linear(256, 2304), nn.ReLU(), nn.Linear(2304, 256), nn.ReLU(),
+            nn.Linear(256, 1024, bias=False), nn.ReLU(), nn.Linear(1024, 256),
+        )
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def awq_b128_inputs():
+    """bf16 MLP + calibration batches of the INT4_AWQ_CFG (block 128) golden: channels of the input
+    carry per-column gains (0.25 .. 8) so act_scale varies across K, M = 192 rows per batch (a
+    tail below the 256-row tile)."""
+    torch.manual_seed(73)
+    model = _WideMLP().to(torch.bfloat16)
+    g = torch.Generator().manual_seed(71)
+    gain = torch.exp2(torch.rand(256, generator=g) * 5 - 2)
+    data = [(torch.randn(2, 96, 256, generator=g) * gain).to(torch.bfloat16) for _ in range(3)]
+    test = (torch.randn(2, 32, 256, generator=g) * gain).to(torch.bfloat16)
+    return model, data, test
+
+
+def gen_awq_b128():
+    """C3's real search path: mtq.INT4_AWQ_CFG (awq_lite, block 128, alpha step 0.1) in bf16 on
+    linears that qualify for the fast search (K % 64 == 0) -- the product's fused-MFMA and
+    batched paths are pinned against this run of the reference."""
+    model, data, test = awq_b128_inputs()
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    import copy
+
+    cfg = copy.deepcopy(mtq.INT4_AWQ_CFG)
+    cfg["algorithm"] = {"method": "awq_lite", "alpha_step": 0.1, "debug": True}
+
+    def loop(mm):
+        for d in data:
+            mm(d)
+
+    mtq.quantize(model, cfg, loop)
+    t = {f"sd.{k}": v for k, v in sd.items()}
+    for i, d in enumerate(data):
+        t[f"data{i}"] = d
+    meta = {"cfg_algorithm": cfg["algorithm"], "threads": torch.get_num_threads()}
+    for n, m in model.named_modules():
+        if hasattr(m, "awq_lite"):
+            t[f"best_scale.{n}"] = m.awq_lite.best_scale.clone()
+            t[f"act_scale.{n}"] = m.awq_lite.act_scale.clone()
+            t[f"weight_scale.{n}"] = m.awq_lite.weight_scale.clone()
+            t[f"weight.{n}"] = m.weight.detach().clone()
+            t[f"wamax.{n}"] = m.weight_quantizer.amax.clone()
+            t[f"pqs.{n}"] = m.input_quantizer.pre_quant_scale.clone()
+            meta[n] = {"best_alpha": m.awq_lite.best_alpha,
+                       "loss": {str(k): float(v) for k, v in m.awq_lite.loss.items()},
+                       "N": m.weight.shape[0], "K": m.weight.shape[1]}
+    t["test"] = test
+    t["out"] = model(test).detach()
+    save_file(t, str(OUT / "awq_b128.safetensors"))
+    (OUT / "awq_b128.json").write_text(json.dumps(meta, indent=1))
 
 
 def gen_nvfp4():

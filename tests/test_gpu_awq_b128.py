@@ -1,0 +1,108 @@
+"""C3's real AWQ-lite search path against the reference (INT4_AWQ_CFG, block 128, bf16).
+
+Golden: ``tests/golden/awq_b128.*`` -- the reference's ``mtq.quantize(model, INT4_AWQ_CFG)`` run on
+the CPU (``make_golden.py gen_awq_b128``) on a bf16 MLP whose linears all take the product's fast
+search (K % 64 == 0): N = 2304 goes to the batched hipBLASLt search under ``auto``, N = 256 / 1024 to
+the fused MFMA search kernel (csrc/mtq_awq_gemm.hip), and ``never`` runs the per-alpha path
+(reference model_calib.py:1513-1560 restated one alpha at a time).
+
+Bounds (GEMM summation order differs between the reference's CPU run and the GPU):
+* best alpha per linear: equal (the reference's losses are >= 1.3 % apart at the minimum);
+* per-alpha losses: rtol 2e-2 (bf16 outputs of differently ordered fp32 sums);
+* act_scale: bf16 ``mean(|x|)`` -- within 2 bf16 ulps (rtol 2^-7); best_scale (fp32) rtol 2e-2;
+* folded weights ``bf16(W / s)`` and block amax: rtol 2e-2, and at least 99 % of the weight elements
+  bit-identical;
+* outputs of the quantized model: rtol 5e-2 / atol 5e-2 on a bf16 4-layer MLP.
+"""
+
+from pathlib import Path
+
+import json
+
+import pytest
+import torch
+import torch.nn as nn
+from safetensors.torch import load_file
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+
+
+class _WideMLP(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.net = nn.Sequential(
+            nn.Linear(256, 2304), nn.ReLU(), nn.Linear(2304, 256), nn.ReLU(),
+            nn.Linear(256, 1024, bias=False), nn.ReLU(), nn.Linear(1024, 256),
+        )
+
+    def forward(self, x):
+        return self.net(x)
+
+
+def _run(gpu, mode, alpha_step=0.1):
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization import model_calib
+
+    t = load_file(str(G / "awq_b128.safetensors"))
+    model = _WideMLP().to(torch.bfloat16)
+    model.load_state_dict({k[3:]: v for k, v in t.items() if k.startswith("sd.")})
+    model.to(gpu)
+    data = [t[f"data{i}"].to(gpu) for i in range(3)]
+    cfg = dict(mtq.INT4_AWQ_CFG)
+    cfg["algorithm"] = {"method": "awq_lite", "alpha_step": alpha_step, "debug": True}
+
+    def loop(mm):
+        for d in data:
+            mm(d)
+
+    old = model_calib._AWQ_FUSED
+    model_calib._AWQ_FUSED = mode
+    try:
+        mtq.quantize(model, cfg, loop)
+    finally:
+        model_calib._AWQ_FUSED = old
+    return model, t
+
+
+@pytest.mark.parametrize("mode", ["auto", "always", "never"])
+def test_awq_lite_int4_b128_matches_reference(gpu, mode):
+    model, t = _run(gpu, mode)
+    meta = json.loads((G / "awq_b128.json").read_text())
+    seen = 0
+    for n, m in model.named_modules():
+        if not hasattr(m, "awq_lite"):
+            continue
+        seen += 1
+        h = m.awq_lite
+        ref_loss = torch.tensor([meta[n]["loss"][k] for k in sorted(meta[n]["loss"], key=float)])
+        got_loss = torch.tensor([h.loss[a] for a in sorted(h.loss)])
+        torch.testing.assert_close(got_loss, ref_loss, rtol=2e-2, atol=0, msg=lambda s: f"{n} loss: {s}")
+        assert h.best_alpha == pytest.approx(meta[n]["best_alpha"]), n
+        torch.testing.assert_close(h.act_scale.float().cpu(), t[f"act_scale.{n}"].float(), rtol=2**-7, atol=0)
+        torch.testing.assert_close(h.best_scale.cpu(), t[f"best_scale.{n}"], rtol=2e-2, atol=0)
+        w, wr = m.weight.detach().cpu(), t[f"weight.{n}"]
+        torch.testing.assert_close(w, wr, rtol=2e-2, atol=1e-6)
+        same = (w.view(torch.int16) == wr.view(torch.int16)).float().mean().item()
+        assert same >= 0.99, (n, same)
+        torch.testing.assert_close(m.weight_quantizer.amax.float().cpu(), t[f"wamax.{n}"].float(), rtol=2e-2, atol=0)
+        torch.testing.assert_close(m.input_quantizer.pre_quant_scale.float().cpu(), t[f"pqs.{n}"].float(),
+                                   rtol=2e-2, atol=0)
+    assert seen == 4
+    out = model(t["test"].to(gpu)).detach().cpu()
+    torch.testing.assert_close(out.float(), t["out"].float(), rtol=5e-2, atol=5e-2)
+
+
+def test_awq_lite_fine_alpha_grid_falls_back(gpu):
+    """alpha_step 0.01 = 101 alphas: more than the fused search kernel's 64 and the batched path's
+    16; the search must fall to a path that takes any alpha count (the reference takes any step)
+    and pick the same alpha under every mode."""
+    best = {}
+    for mode in ("auto", "always", "never"):
+        model, _ = _run(gpu, mode, alpha_step=0.01)
+        for n, m in model.named_modules():
+            if hasattr(m, "awq_lite"):
+                assert len(m.awq_lite.loss) == 101
+                best.setdefault(n, []).append(m.awq_lite.best_alpha)
+    for n, b in best.items():
+        assert max(b) - min(b) <= 0.0100001, (n, b)

@@ -1,0 +1,66 @@
+"""HistogramCalibrator on the GPU against the reference run at > 2^24 counts per call.
+
+Golden ``tests/golden/calib_ref.*`` (``make_golden.py gen_calib_ref``): the reference's
+``HistogramCalibrator.collect`` (calib/histogram.py:77-130, torch.histc's fp32 counts) on two
+40 M-element peaked bf16 tensors (``hist_inputs.peaked``: one bin past 2^24 in each call) with 1
+and 3 intra-op threads and with skip_zeros, then ``compute_amax`` (entropy / percentile / MSE).
+The product sets the same thread count (``torch.set_num_threads``), counts each thread's chunk
+exactly on the GPU and folds them as histc does: histograms and amax must be bit-equal.  The
+small-batch MSE cases pin the MSE sweep's actual call (``bias = num_bits``).
+"""
+
+import json
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+sys.path.insert(0, str(G))
+
+
+def test_histogram_calibrator_matches_reference_above_2p24(gpu):
+    from hist_inputs import peaked
+    from modelopt_amd.torch.quantization.calib import HistogramCalibrator
+
+    t = load_file(str(G / "calib_ref.safetensors"))
+    meta = json.loads((G / "calib_ref.json").read_text())
+    saved = torch.get_num_threads()
+    try:
+        for c in meta["cases"]:
+            torch.set_num_threads(c["threads"])
+            h = HistogramCalibrator(8, None, False, num_bins=2048, skip_zeros=c["skip_zeros"])
+            for scale in (1.0, 1.5):
+                h.collect(peaked(scale=scale, zeros_every=4 if c["skip_zeros"] else 0).to(gpu))
+            assert h._num_bins == c["num_bins"], c["key"]
+            got = h._calib_hist.cpu()
+            want = t[f"hist_{c['key']}"]
+            assert torch.equal(h._calib_bin_edges.cpu(), t[f"edges_{c['key']}"]), c["key"]
+            assert torch.equal(got, want), (c["key"], (got - want).abs().max().item())
+            assert float(got.max()) == c["max_count"]
+            assert float(h.compute_amax("percentile", percentile=99.99)) == c["percentile_9999"], c["key"]
+            assert float(h.compute_amax("mse")) == c["mse"], c["key"]
+            if "entropy" in c:
+                assert float(h.compute_amax("entropy")) == c["entropy"], c["key"]
+    finally:
+        torch.set_num_threads(saved)
+
+
+def test_histogram_mse_small_batches_match_reference(gpu):
+    from modelopt_amd.torch.quantization.calib import HistogramCalibrator
+
+    meta = json.loads((G / "calib_ref.json").read_text())
+    g = torch.Generator().manual_seed(20)
+    xs = [torch.randn(32, 64, generator=g) * s for s in (1.0, 2.5, 0.7)]
+    for nb, u in [(8, False), (8, True), (4, False)]:
+        h = HistogramCalibrator(nb, None, u, num_bins=256)
+        for x in xs:
+            h.collect((x.abs() if u else x).to(gpu))
+        assert float(h.compute_amax("mse", start_bin=16)) == meta[f"small_mse_b{nb}_u{int(u)}"], (nb, u)
+    h = HistogramCalibrator((4, 3), None, False, num_bins=256)
+    h.collect(xs[0].to(gpu))
+    with pytest.raises(TypeError):
+        h.compute_amax("mse", start_bin=16)
