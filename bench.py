@@ -246,6 +246,11 @@ def cpu_baseline(target_s: float = 10.0):
         "kind": "port",
         "sample": f"{passes} passes of FP8 e4m3 static block-128 fake-quant (oracle fp8_eager, the "
         f"reference _fp8_eager ATen sequence) over bf16 [{rows}, {HIDDEN}], {el:.1f} s, {nt} threads",
+        "cores_basis": (
+            f"torch intra-op threads = {nt} (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}): "
+            f"the job's CPU share on the shared GPU box, not the host's {info['host_physical_cores']} "
+            f"physical cores ({info['process_cpus']} CPUs in the affinity mask are shared with other jobs)"
+        ),
         "one_thread": {
             "value": round(p1 * xs1.numel() / el1 / 1e9, 4),
             "unit": "G-elem/s",
