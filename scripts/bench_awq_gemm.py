@@ -1,9 +1,18 @@
 #!/usr/bin/env python3
-"""AWQ-lite alpha search per linear, Llama-3-8B shapes, one calibration batch (8192 tokens):
-fused MFMA search (block_quant_dynamic_multi + awq_search_gemm, all 11 alphas) vs the unfused
-per-alpha path (block_quant_dynamic, mul_cols, hipBLASLt F.linear, mse_accumulate).
-Reports ms per linear and the search GEMM's TFLOP/s (2*M*N*K*G / kernel time) vs 2.5 PF."""
+"""AWQ-lite alpha search per linear, Llama-3-8B shapes, one calibration batch (8192 tokens, 11
+alphas), all in one process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24):
+
+* ``pp``      -- mtq_awq_search_gemm mode 2 (r03 ping-pong kernel + pre-scale pass), weights cached
+* ``r02``     -- mode 1 (r02 kernel, x scaled while register-staged)
+* ``batched`` -- the r02 wide-linear path: awq_prescale + 11 hipBLASLt torch.mm into [G, M, N] +
+                 awq_mse_multi
+* ``per_alpha`` -- the r01 path: per alpha mul_cols + hipBLASLt F.linear + mse_accumulate
+* ``hipblaslt_gemms`` -- the 11 bf16 GEMMs alone
+Reports ms (median over rounds) and TFLOP/s = 2*M*N*K*G / time vs the 2.5 PF dense bf16 peak.
+Usage: bench_awq_gemm.py [M] [rounds]"""
 import json
+import os
+import statistics
 import sys
 from pathlib import Path
 
@@ -16,11 +25,13 @@ from modelopt_amd import _ext  # noqa: E402
 
 ops = _ext.ops()
 dev = torch.device("cuda")
-M, G = int(sys.argv[1]) if len(sys.argv) > 1 else 8192, 11
-SHAPES = {"q_proj": (4096, 4096), "k_proj": (1024, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
+M = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+G = 11
+SHAPES = {"k_proj": (1024, 4096), "q_proj": (4096, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
 
 
-def timeit(fn, iters=5):
+def timeit(fn, iters=3):
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -30,6 +41,13 @@ def timeit(fn, iters=5):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / iters
+
+
+def with_mode(mode, fn):
+    def run():
+        os.environ["MTQ_AMD_AWQ_GEMM_MODE"] = str(mode)
+        fn()
+    return run
 
 
 res = {}
@@ -43,30 +61,41 @@ for name, (N, K) in SHAPES.items():
     loss = torch.zeros(G, device=dev)
     wq = ops.block_quant_dynamic_multi(w, pw, 128, 4, False, False)
 
-    def fused():
-        wq2 = ops.block_quant_dynamic_multi(w, pw, 128, 4, False, False)
-        ops.awq_search_gemm(x, si, wq2, None, yref, loss)
-
-    def gemm_only():
+    def search():
         ops.awq_search_gemm(x, si, wq, None, yref, loss)
 
-    def unfused():
+    def batched():
+        xs = ops.awq_prescale(x, si)
+        out = torch.empty((G, M, N), dtype=x.dtype, device=dev)
         for g in range(G):
-            wqg = ops.block_quant_dynamic(w, pw[g], 128, 4, False, False)
-            out = F.linear(ops.mul_cols(x, si[g]), wqg)
+            torch.mm(xs[g], wq[g].t(), out=out[g])
+        ops.awq_mse_multi(out, yref, loss)
+
+    def per_alpha():
+        for g in range(G):
+            out = F.linear(ops.mul_cols(x, si[g]), wq[g])
             ops.mse_accumulate(out, yref, loss, g)
 
-    def hipblaslt_only():
+    def hipblaslt_gemms():
         for g in range(G):
             F.linear(x, wq[g])
 
+    arms = {"pp": with_mode(2, search), "r02": with_mode(1, search), "batched": batched,
+            "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
+    t = {k: [] for k in arms}
+    for _ in range(ROUNDS):
+        for k, f in arms.items():
+            t[k].append(timeit(f))
     flops = 2.0 * M * N * K * G
-    r = {k: round(timeit(f), 3) for k, f in
-         (("fused_ms", fused), ("search_gemm_ms", gemm_only), ("unfused_ms", unfused), ("hipblaslt_gemms_ms", hipblaslt_only))}
-    r["search_gemm_tflops"] = round(flops / (r["search_gemm_ms"] * 1e-3) / 1e12, 1)
-    r["hipblaslt_tflops"] = round(flops / (r["hipblaslt_gemms_ms"] * 1e-3) / 1e12, 1)
-    r["search_gemm_frac_of_2.5PF"] = round(r["search_gemm_tflops"] / 2500, 3)
-    r["speedup_vs_unfused"] = round(r["unfused_ms"] / r["fused_ms"], 3)
+    r = {}
+    for k, v in t.items():
+        ms = statistics.median(v)
+        r[k] = {"ms": round(ms, 3), "min_ms": round(min(v), 3), "tflops": round(flops / (ms * 1e-3) / 1e12, 1)}
+        r[k]["frac_of_2.5PF"] = round(r[k]["tflops"] / 2500, 3)
+    r["pp_speedup_vs_batched"] = round(r["batched"]["ms"] / r["pp"]["ms"], 3)
+    r["pp_speedup_vs_per_alpha"] = round(r["per_alpha"]["ms"] / r["pp"]["ms"], 3)
+    r["pp_speedup_vs_r02"] = round(r["r02"]["ms"] / r["pp"]["ms"], 3)
     res[name] = r
-    print(name, r, file=sys.stderr, flush=True)
-print(json.dumps({"M": M, "G": G, "shapes": res}))
+    print(name, json.dumps(r), file=sys.stderr, flush=True)
+os.environ.pop("MTQ_AMD_AWQ_GEMM_MODE", None)
+print(json.dumps({"M": M, "G": G, "rounds": ROUNDS, "shapes": res}))

@@ -202,6 +202,12 @@ def sync_sharded_amax(model: nn.Module, device=None, group=None) -> int:
     host objects; the values travel in ONE packed fp32 ``all_reduce(MAX)`` on ``device`` (RCCL on
     MI355X; host-staged under gloo).  Static block weight quantizers are then promoted on every
     rank.  Returns the number of entries in the packed buffer.
+
+    Requirement: the layers a rank does not own hold their parameters on the meta device (as
+    ``layer_sharded_calibration`` runs them).  A stage owner's AWQ / SmoothQuant calibration folds
+    ``1 / pre_quant_scale`` into ITS weights; a non-owner with real, unfolded weights would get the
+    owner's ``pre_quant_scale`` and amax on top of them, so receiving a ``_pre_quant_scale`` into a
+    module with real parameters raises.
     """
     if not (dist.is_available() and dist.is_initialized()):
         return 0
@@ -241,6 +247,16 @@ def sync_sharded_amax(model: nn.Module, device=None, group=None) -> int:
         flat = c.to(device)
     else:
         dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=group)
+    named = dict(model.named_modules())
+    for name, attr in keys:
+        if attr != "_pre_quant_scale" or (name, attr) in mine or name not in mods:
+            continue
+        parent = named.get(name.rsplit(".", 1)[0]) if "." in name else model
+        if parent is not None and any(p.device.type != "meta" for p in parent.parameters(recurse=False)):
+            raise RuntimeError(
+                f"sync_sharded_amax: {name} receives another rank's pre_quant_scale but its module holds "
+                "real weights; non-owned layers must be on the meta device (the owner folded 1/s into its own)"
+            )
     off = 0
     for k, sz in zip(keys, sizes):
         (name, attr), (shape, dt) = k, layout[k]

@@ -11,6 +11,8 @@ and raise for the other formats.
 
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd import Function
 
@@ -75,15 +77,21 @@ def dynamic_block_quantize_op(
     )
 
 
-def _register_reference_op_names() -> bool:
-    """Register the reference's own op names -- ``tensorrt::quantize_op``,
+def register_reference_op_names() -> bool:
+    """Opt-in (call it, or set ``MTQ_AMD_REGISTER_TENSORRT_OPS=1`` before import): register the
+    reference's own op names -- ``tensorrt::quantize_op``,
     ``tensorrt::dynamic_block_quantize_op`` and its ``.overload`` (None amax), schemas of
     tensor_quant.py:222-237 -- on the CUDA (= HIP), CPU and Meta keys, so code that calls
     ``torch.ops.tensorrt.*`` directly (or a torch.export graph holding them) runs on these
     kernels.  The ``.overload`` computes the quantization (the reference's implementation of it
     returns ``torch.empty_like(input)``, tensor_quant.py:240-249, uninitialised memory).  When the
     reference package already defined the namespace in this process, its registration stays and
-    nothing is replaced (returns False)."""
+    nothing is replaced (returns False).  Not done by default: once taken here, a reference
+    package imported later in the same process would find its namespace defined, swallow the
+    error and silently dispatch to these kernels."""
+    global REFERENCE_OP_NAMES_REGISTERED
+    if REFERENCE_OP_NAMES_REGISTERED:
+        return True
     try:
         lib = torch.library.Library("tensorrt", "FRAGMENT")
         lib.define(
@@ -119,11 +127,14 @@ def _register_reference_op_names() -> bool:
     for name in ("quantize_op", "dynamic_block_quantize_op", "dynamic_block_quantize_op.overload"):
         lib.impl(name, _fake, "Meta")
     _REFERENCE_OP_LIB.append(lib)  # keep the registration alive
+    REFERENCE_OP_NAMES_REGISTERED = True
     return True
 
 
 _REFERENCE_OP_LIB: list = []
-REFERENCE_OP_NAMES_REGISTERED = _register_reference_op_names()
+REFERENCE_OP_NAMES_REGISTERED = False
+if os.environ.get("MTQ_AMD_REGISTER_TENSORRT_OPS", "0") == "1":
+    register_reference_op_names()
 
 
 def e4m3_cast(x):

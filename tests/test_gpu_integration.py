@@ -93,6 +93,7 @@ def test_integration_stub_reports_errors(gpu):
 def test_reference_op_names_on_device(gpu):
     from modelopt_amd.torch.quantization import tensor_quant as tq
 
+    assert tq.register_reference_op_names()  # opt-in
     assert tq.REFERENCE_OP_NAMES_REGISTERED
     g = torch.Generator().manual_seed(3)
     x = (torch.randn(64, 256, generator=g) * 2).to(torch.bfloat16)
