@@ -68,9 +68,28 @@ class _QuantFusedExperts(QuantModule):
         orig_linear = torch.nn.functional.linear
         first_in = getattr(self, f"{self._first_proj_attr}_input_quantizer")
         first_w = getattr(self, f"{self._first_proj_attr}_weight_quantizers")
+        d = self.__dict__
+        d["_first_in_done"] = False
+        # The first projection's input of expert e is hidden_states[token_idx_e]: when every token
+        # is routed to some expert and the shared input quantizer acts on each token on its own,
+        # applying it ONCE to hidden_states (collect and/or fake quant) equals applying it to each
+        # expert's gather -- max over the union = max of the per-expert maxima, and a per-element
+        # qdq commutes with the gather -- so one reduction / qdq launch replaces E of them.
+        args = list(args)
+        hs = args[0] if args else kwargs.get("hidden_states")
+        idx_t = args[1] if len(args) > 1 else kwargs.get("top_k_index")
+        if (
+            isinstance(hs, torch.Tensor) and hs.dim() == 2 and isinstance(idx_t, torch.Tensor)
+            and _token_separable(first_in) and bool((idx_t < self.num_experts).all())
+        ):
+            hs = first_in(hs)
+            if args:
+                args[0] = hs
+            else:
+                kwargs["hidden_states"] = hs
+            d["_first_in_done"] = True
 
         def _quantized_linear(input, weight, bias=None):
-            d = self.__dict__
             if d["_down_proj_linear"]:
                 idx = d["_current_expert_idx"]
                 input = self.down_proj_input_quantizer(input)
@@ -78,12 +97,13 @@ class _QuantFusedExperts(QuantModule):
             else:
                 idx = self._get_expert_idx_from_first_proj(weight)
                 d["_current_expert_idx"] = idx
-                input = first_in(input)
+                if not d["_first_in_done"]:
+                    input = first_in(input)
                 weight = first_w[idx](weight)
             d["_down_proj_linear"] = not d["_down_proj_linear"]
             return orig_linear(input, weight, bias)
 
-        self.__dict__["_down_proj_linear"] = False
+        d["_down_proj_linear"] = False
         with _replace_function(torch.nn.functional, "linear", _quantized_linear):
             return self._original_cls.forward(self, *args, **kwargs)
 
@@ -101,6 +121,36 @@ class _QuantFusedExperts(QuantModule):
         for w, q in self.iter_weights_for_calibration():
             if isinstance(q, TensorQuantizer) and q.fake_quant:
                 self._fold_weight_quantizer(q, (w,), keep_attrs)
+
+
+def _token_separable(q) -> bool:
+    """Whether ``q`` treats every row (token) of a [tokens, H] input on its own, so that applying
+    it to all tokens at once equals applying it to any cover of the tokens by row subsets: disabled;
+    or collecting into a MaxCalibrator per tensor / per last-dim channel; and quantizing with a
+    static per-tensor / per-last-dim amax or dynamic blocks along the last dim only (MX, NVFP4,
+    per-token FP8).  Anything else (dynamic per-tensor amax, static row blocks, histograms,
+    custom backends) keeps the per-expert calls."""
+    from ..calib.max import MaxCalibrator
+
+    if type(q) is not TensorQuantizer:
+        return False
+    if q._disabled:
+        return True
+    if getattr(q, "backend", None) is not None:
+        return False
+    last_axis = q.axis is None or q.axis in (-1, 1, (-1,), (1,), [-1], [1])
+    if q._if_calib and not q._dynamic:
+        if type(q._calibrator) is not MaxCalibrator or not last_axis:
+            return False
+    if q._if_quant:
+        bs = q.block_sizes
+        if bs:
+            dims = [k for k in bs if isinstance(k, int)]
+            if bs.get("type") != "dynamic" or any(k not in (-1, 1) for k in dims):
+                return False
+        elif q._dynamic or not last_axis:
+            return False
+    return True
 
 
 def _has_num_experts(obj) -> bool:
