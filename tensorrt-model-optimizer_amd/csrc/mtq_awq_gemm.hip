@@ -368,8 +368,13 @@ template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T, bool HAS_BIAS>
+// PROBE (measurement builds only, MTQ_AMD_AWQ_GEMM_PROBE=1): no global loads in the K loop -- the
+// ds_read + MFMA + barrier skeleton alone (the loss is then meaningless)
+// V (A/B of code shapes): bit 0 = transposed MFMA (out^T accumulators, W fragment as the A operand),
+// bit 1 = the last K tile re-loads itself (no branch in the loop) instead of skipping its loads
+template <typename T, bool HAS_BIAS, int PH, int PROBE = 0, int EPI = 0, int V = 1>
 __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) {
+  constexpr bool TRANS = V & 1, CLAMP = (V >> 1) & 1;
   using namespace pp;
   typedef typename Mfma16<T>::v8 v8;
   __shared__ __attribute__((aligned(16))) unsigned char lds[kLds];
@@ -447,88 +452,243 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (int)(K / kBK);
-  // prologue: K tile 0 in full; phase 0 needs A0 and B0 (issued first)
+  // prologue: K tile 0 in full (A0 B0 B1 A1); phase 0 needs A0 and B0 (PH 4) or A0, B0, B1 (PH 2)
 #pragma unroll
   for (int q = 0; q < 4; ++q) load_half(q, lds, 0);
-  wait_vm<4>();
+  if constexpr (PH == 4)
+    wait_vm<4>();
+  else
+    wait_vm<2>();
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger (wave-uniform: scalar branch)
 
-  v8 af[4][2], bf[2][2];
-  for (int t = 0; t < nt; ++t) {
-    unsigned char *cur = lds + (t & 1) * kBuf;
-    unsigned char *nxt = lds + ((t + 1) & 1) * kBuf;
-    const int64_t kn = (int64_t)(t + 1 < nt ? t + 1 : nt - 1) * kBK;  // last tile: a harmless re-load
+  if constexpr (PH == 4) {
+    v8 af[4][2], bf[2][2];
+    for (int t = 0; t < nt; ++t) {
+      unsigned char *cur = lds + (t & 1) * kBuf;
+      unsigned char *nxt = lds + ((t + 1) & 1) * kBuf;
+      const int64_t kn = (int64_t)(CLAMP ? (t + 1 < nt ? t + 1 : nt - 1) : t + 1) * kBK;
+      const bool more = PROBE == 0 && (CLAMP || t + 1 < nt);  // the last tile loads nothing and drains
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int mq = (q == 0 || q == 1) ? 0 : 1;
-      const int nq = (q == 1 || q == 2) ? 1 : 0;
-      if (q == 0 || q == 2) {
+      for (int q = 0; q < 4; ++q) {
+        const int mq = (q == 0 || q == 1) ? 0 : 1;
+        const int nq = (q == 1 || q == 2) ? 1 : 0;
+        if (q == 0 || q == 2) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i][s] = read_a(cur, 4 * mq + i, s);
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) af[i][s] = read_a(cur, 4 * mq + i, s);
+          for (int j = 0; j < 2; ++j) bf[j][s] = read_b(cur, 2 * nq + j, s);
+        if (more) {
+          load_half(q, nxt, kn);
+          if (q == 2)
+            wait_vm<6>();
+          else
+            wait_vm<4>();
+        } else {
+          wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+        if constexpr (TRANS) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)  // the A operand (W fragment) held for 4 MFMAs
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bf[j][s], af[i][s], acc[4 * mq + i][2 * nq + j]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(af[i][s], bf[j][s], acc[4 * mq + i][2 * nq + j]);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
       }
+    }
+  } else {
+    // PH == 2: two phases per K tile, one m-quadrant (32 MFMAs) each -- half the barriers.
+    // Phase 0 reads the m0 A fragments and ALL B fragments (kept for phase 1) and issues A0, B0,
+    // B1 of the next tile (their last readers were two phases back); phase 1 reads the m1 A
+    // fragments and issues A1.  Waits: after phase 0's six loads, phase 1 needs A1 of this tile
+    // (issued a tile earlier) -> vmcnt(6); after phase 1's two, the next phase needs A0/B0/B1 of
+    // the next tile -> vmcnt(2).
+    v8 af[4][2], bf[4][2];
+    for (int t = 0; t < nt; ++t) {
+      unsigned char *cur = lds + (t & 1) * kBuf;
+      unsigned char *nxt = lds + ((t + 1) & 1) * kBuf;
+      const int64_t kn = (int64_t)(t + 1) * kBK;
+      const bool more = t + 1 < nt;
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int ph = 0; ph < 2; ++ph) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j][s] = read_b(cur, 2 * nq + j, s);
-      load_half(q, nxt, kn);
-      if (q == 2)
-        wait_vm<6>();
-      else
-        wait_vm<4>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_setprio(1);
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+          for (int i = 0; i < 4; ++i) af[i][s] = read_a(cur, 4 * ph + i, s);
+        if (ph == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(af[i][s], bf[j][s], acc[4 * mq + i][2 * nq + j]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
+            for (int j = 0; j < 4; ++j) bf[j][s] = read_b(cur, j, s);
+          if (more) {
+            load_half(0, nxt, kn);
+            load_half(1, nxt, kn);
+            load_half(2, nxt, kn);
+            wait_vm<6>();
+          } else {
+            wait_vm<0>();
+          }
+        } else {
+          if (more) {
+            load_half(3, nxt, kn);
+            wait_vm<2>();
+          } else {
+            wait_vm<0>();
+          }
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc[4 * ph + i][j] = Mfma16<T>::mma(bf[j][s], af[i][s], acc[4 * ph + i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+      }
     }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-  wait_vm<0>();  // the last tile's re-loads land before the LDS is reused
-  __syncthreads();
 
-  // ---- epilogue: yref tile [256 x 256] into LDS (16 DMA rounds in flight), then the loss
-  const T *Y = reinterpret_cast<const T *>(p.yref);
-  {
-    const int ck = tid & 31;
-    int64_t col = n0 + ck * 8;
-    col = col < p.N ? col : p.N - 8;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      int64_t row = m0 + u * 16 + (tid >> 5);
-      row = row < p.M ? row : p.M - 1;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
-                                       (__attribute__((address_space(3))) void *)(lds + u * 8192 + wave * 1024),
-                                       16, 0, 0);
-    }
-  }
-  wait_vm<0>();
-  __syncthreads();
   float sum = 0.f;
+  if constexpr (TRANS) {
+  // ---- epilogue.  The MFMAs computed out^T (W fragment as the A operand), so a lane's four
+  // accumulators of tile (i, j) are out[m][n .. n+3] with m = 16 i + (lane & 15), n = 16 j +
+  // 4 (lane >> 4): the reference rows come straight from HBM as one 8-byte load each (no LDS
+  // staging, no barrier), all 32 issued before the first use.  Bias, output and difference
+  // rounded to T, fp32 square-sum in a fixed order.
+  const T *Y = reinterpret_cast<const T *>(p.yref);
   const T *Bi = reinterpret_cast<const T *>(p.bias);
+  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+  u32x2_t yv[8][4];
+  bool rok[8], cok[4];
+  int64_t coln[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int cl = wn * 64 + 16 * j + fr;
-    const bool cok = n0 + cl < p.N;
-    float bj = 0.f;
-    if (HAS_BIAS) bj = Elem<T>::ld(Bi[cok ? n0 + cl : p.N - 1]);
+    const int64_t c = n0 + wn * 64 + 16 * j + 4 * fq;
+    cok[j] = c < p.N;  // N % 8 == 0: the 4 columns are all in or all out
+    coln[j] = cok[j] ? c : p.N - 4;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rok[i] = m0 + grp * 128 + 16 * i + fr < p.M;
+  if constexpr (EPI == 1) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      int64_t r = m0 + grp * 128 + 16 * i + fr;
+      r = rok[i] ? r : p.M - 1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yv[i][j] = *reinterpret_cast<const u32x2_t *>(Y + r * p.N + coln[j]);
+    }
+  } else {
+    // the yref tile [256 x 256] through LDS: 16 DMA rounds in flight, row r's 16-byte chunk c
+    // stored at chunk c ^ (r & 15) (source-side XOR), so the 16 rows of a b64 read hit 16 slots
+    wait_vm<0>();
+    __syncthreads();
+    {
+      const int slot = tid & 31;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int rr = u * 16 + (tid >> 5);
+        int64_t row = m0 + rr;
+        row = row < p.M ? row : p.M - 1;
+        int64_t col = n0 + (int64_t)((slot ^ (rr & 15)) * 8);
+        col = col < p.N ? col : p.N - 8;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
+                                         (__attribute__((address_space(3))) void *)(lds + u * 8192 + wave * 1024),
+                                         16, 0, 0);
+      }
+    }
+    wait_vm<0>();
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rr = grp * 128 + 16 * i + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cl = wn * 64 + 16 * j + 4 * fq;
+        yv[i][j] = *reinterpret_cast<const u32x2_t *>(lds + rr * 512 + (((cl >> 3) ^ (rr & 15)) << 4) + (cl & 7) * 2);
+      }
+    }
+  }
+  float bj[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bj[j][e] = HAS_BIAS ? Elem<T>::ld(Bi[coln[j] + e]) : 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      T yr[4];
+      __builtin_memcpy(yr, &yv[i][j], 8);
+      const bool ok = rok[i] && cok[j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int rl = grp * 128 + 16 * i + 4 * fq + e;
-        const T yr = *reinterpret_cast<const T *>(lds + rl * 512 + cl * 2);
-        const float y = Elem<T>::ld(Elem<T>::st(acc[i][j][e] + bj));
-        const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr)));
-        sum = (cok && m0 + rl < p.M) ? __builtin_fmaf(d, d, sum) : sum;
+        const float y = Elem<T>::ld(Elem<T>::st(acc[i][j][e] + bj[j][e]));
+        const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr[e])));
+        sum = ok ? __builtin_fmaf(d, d, sum) : sum;
+      }
+    }
+  }
+  } else {
+    // original orientation: lane holds out[16 i + 4 (lane >> 4) + e][16 j + (lane & 15)]; the
+    // reference tile through LDS (plain [256][256] image) read back per element
+    wait_vm<0>();
+    __syncthreads();
+    const T *Y = reinterpret_cast<const T *>(p.yref);
+    const T *Bi = reinterpret_cast<const T *>(p.bias);
+    {
+      const int ck = tid & 31;
+      int64_t col = n0 + ck * 8;
+      col = col < p.N ? col : p.N - 8;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        int64_t row = m0 + u * 16 + (tid >> 5);
+        row = row < p.M ? row : p.M - 1;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
+                                         (__attribute__((address_space(3))) void *)(lds + u * 8192 + wave * 1024),
+                                         16, 0, 0);
+      }
+    }
+    wait_vm<0>();
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cl = wn * 64 + 16 * j + fr;
+      const bool cok = n0 + cl < p.N;
+      float bj = 0.f;
+      if (HAS_BIAS) bj = Elem<T>::ld(Bi[cok ? n0 + cl : p.N - 1]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rl = grp * 128 + 16 * i + 4 * fq + e;
+          const T yr = *reinterpret_cast<const T *>(lds + rl * 512 + cl * 2);
+          const float y = Elem<T>::ld(Elem<T>::st(acc[i][j][e] + bj));
+          const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr)));
+          sum = (cok && m0 + rl < p.M) ? __builtin_fmaf(d, d, sum) : sum;
+        }
       }
     }
   }
@@ -683,11 +843,8 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
   }
   AwqGemmArgs a{xa, sinv, wq, bias, yref, workspace, M, N, K, (int)tiles_m, (int)tiles_n, G};
   const dim3 grid((unsigned)(tiles * G));
-  static int probe = -1;
-  if (probe < 0) {
-    const char *e = getenv("MTQ_AMD_AWQ_GEMM_PROBE");
-    probe = e ? atoi(e) : 0;
-  }
+  const char *pe_ = getenv("MTQ_AMD_AWQ_GEMM_PROBE");
+  const int probe = pe_ ? atoi(pe_) : 0;
 #define MTQ_AWQ_LAUNCH(TT, PR)                                                                     \
   do {                                                                                             \
     if (probe == 1)                                                                                \
@@ -698,17 +855,41 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
       awq_search_gemm_kernel<TT, PR, 0><<<grid, kThreads, 0, stream>>>(a);                          \
   } while (0)
   if (mode == 2) {
+    const char *pe = getenv("MTQ_AMD_AWQ_PP_PHASES");  // 4 or 2 phases per K tile (A/B switch)
+    const bool ph2 = pe && atoi(pe) == 2;
+    const char *ee = getenv("MTQ_AMD_AWQ_PP_EPI");  // 0: yref through LDS, 1: direct loads (A/B)
+    const int epi = ee ? atoi(ee) : 0;
+    const char *ve = getenv("MTQ_AMD_AWQ_PP_VAR");  // code-shape variant V (A/B), default 1
+    const int var = ve ? atoi(ve) : 1;
+#define MTQ_PP(TT, BB)                                                                              \
+  do {                                                                                             \
+    if (ph2)                                                                                       \
+      awq_search_pp_kernel<TT, BB, 2><<<grid, kThreads, 0, stream>>>(a);                            \
+    else if (probe == 1)                                                                           \
+      awq_search_pp_kernel<TT, BB, 4, 1><<<grid, kThreads, 0, stream>>>(a);                         \
+    else if (epi == 1)                                                                             \
+      awq_search_pp_kernel<TT, BB, 4, 0, 1><<<grid, kThreads, 0, stream>>>(a);                      \
+    else if (var == 0)                                                                             \
+      awq_search_pp_kernel<TT, BB, 4, 0, 0, 0><<<grid, kThreads, 0, stream>>>(a);                   \
+    else if (var == 2)                                                                             \
+      awq_search_pp_kernel<TT, BB, 4, 0, 0, 2><<<grid, kThreads, 0, stream>>>(a);                   \
+    else if (var == 3)                                                                             \
+      awq_search_pp_kernel<TT, BB, 4, 0, 0, 3><<<grid, kThreads, 0, stream>>>(a);                   \
+    else                                                                                           \
+      awq_search_pp_kernel<TT, BB, 4><<<grid, kThreads, 0, stream>>>(a);                            \
+  } while (0)
     if (dtype == MTQ_BF16) {
       if (bias)
-        awq_search_pp_kernel<__bf16, true><<<grid, kThreads, 0, stream>>>(a);
+        MTQ_PP(__bf16, true);
       else
-        awq_search_pp_kernel<__bf16, false><<<grid, kThreads, 0, stream>>>(a);
+        MTQ_PP(__bf16, false);
     } else {
       if (bias)
-        awq_search_pp_kernel<_Float16, true><<<grid, kThreads, 0, stream>>>(a);
+        MTQ_PP(_Float16, true);
       else
-        awq_search_pp_kernel<_Float16, false><<<grid, kThreads, 0, stream>>>(a);
+        MTQ_PP(_Float16, false);
     }
+#undef MTQ_PP
   } else if (dtype == MTQ_BF16) {
     if (pre)
       MTQ_AWQ_LAUNCH(__bf16, true);
