@@ -2,12 +2,12 @@
 """AWQ-lite alpha search per linear, Llama-3-8B shapes, one calibration batch (8192 tokens, 11
 alphas), all in one process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24):
 
-* ``pp``      -- mtq_awq_search_gemm mode 2 (r03 ping-pong kernel + pre-scale pass), weights cached
-* ``pp2``     -- the same with two phases (one m-quadrant, 32 MFMAs) per K tile instead of four
-* ``pp_v0`` / ``pp_v2`` / ``pp_v3`` -- code-shape variants (MTQ_AMD_AWQ_PP_VAR: bit 0 transposed
-  MFMA, bit 1 last-tile re-load instead of a branch); ``pp`` is V = 1
-* ``pp_epi_direct`` -- pp with the reference tile loaded straight into registers (no LDS)
-* ``pp_noload_probe`` -- pp without global loads in the K loop (skeleton timing; wrong losses)
+* ``pp5``     -- mtq_awq_search_gemm mode 2, default schedule 5 (r03 ping-pong kernel + pre-scale
+                 pass; B0 fragments held in registers, every half-tile issued 4-5 phases ahead)
+* ``pp4``     -- schedule 4 (the first r03 schedule, fragments re-read per phase); ``pp4_branch``
+                 the same with the last tile's loads skipped behind a branch (MTQ_AMD_AWQ_PP_CLAMP=0)
+* ``w4``      -- schedule 6: four waves, one per SIMD, 128 x 128 per wave, one barrier per K tile
+* ``*_noload_probe`` -- pp5 / pp4 without global loads in the K loop (skeleton timing; wrong losses)
 * ``r02``     -- mode 1 (r02 kernel, x scaled while register-staged)
 * ``batched`` -- the r02 wide-linear path: awq_prescale + 11 hipBLASLt torch.mm into [G, M, N] +
                  awq_mse_multi
@@ -48,10 +48,9 @@ def timeit(fn, iters=3):
     return e0.elapsed_time(e1) / iters
 
 
-def with_mode(mode, fn, phases=4, probe=0, epi=0, var=1):
+def with_mode(mode, fn, phases=5, probe=0, clamp=1):
     def run():
-        os.environ["MTQ_AMD_AWQ_PP_EPI"] = str(epi)
-        os.environ["MTQ_AMD_AWQ_PP_VAR"] = str(var)
+        os.environ["MTQ_AMD_AWQ_PP_CLAMP"] = str(clamp)
         os.environ["MTQ_AMD_AWQ_GEMM_MODE"] = str(mode)
         os.environ["MTQ_AMD_AWQ_PP_PHASES"] = str(phases)
         os.environ["MTQ_AMD_AWQ_GEMM_PROBE"] = str(probe)
@@ -89,8 +88,9 @@ for name, (N, K) in SHAPES.items():
         for g in range(G):
             F.linear(x, wq[g])
 
-    arms = {"pp": with_mode(2, search), "pp2": with_mode(2, search, 2), "pp_epi_direct": with_mode(2, search, 4, 0, 1),
-            "pp_v0": with_mode(2, search, var=0), "pp_v2": with_mode(2, search, var=2), "pp_v3": with_mode(2, search, var=3), "pp_noload_probe": with_mode(2, search, 4, 1),
+    arms = {"pp5": with_mode(2, search), "pp4": with_mode(2, search, 4),
+            "pp4_branch": with_mode(2, search, 4, clamp=0), "w4": with_mode(2, search, 6),
+            "pp5_noload_probe": with_mode(2, search, 5, 1), "pp4_noload_probe": with_mode(2, search, 4, 1),
             "r02": with_mode(1, search), "batched": batched,
             "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
     t = {k: [] for k in arms}
@@ -103,15 +103,14 @@ for name, (N, K) in SHAPES.items():
         ms = statistics.median(v)
         r[k] = {"ms": round(ms, 3), "min_ms": round(min(v), 3), "tflops": round(flops / (ms * 1e-3) / 1e12, 1)}
         r[k]["frac_of_2.5PF"] = round(r[k]["tflops"] / 2500, 3)
-    r["pp_speedup_vs_batched"] = round(r["batched"]["ms"] / r["pp"]["ms"], 3)
-    r["pp_speedup_vs_per_alpha"] = round(r["per_alpha"]["ms"] / r["pp"]["ms"], 3)
-    r["pp_speedup_vs_r02"] = round(r["r02"]["ms"] / r["pp"]["ms"], 3)
-    r["pp2_speedup_vs_pp"] = round(r["pp"]["ms"] / r["pp2"]["ms"], 3)
+    r["pp5_speedup_vs_batched"] = round(r["batched"]["ms"] / r["pp5"]["ms"], 3)
+    r["pp5_speedup_vs_per_alpha"] = round(r["per_alpha"]["ms"] / r["pp5"]["ms"], 3)
+    r["pp5_speedup_vs_r02"] = round(r["r02"]["ms"] / r["pp5"]["ms"], 3)
+    r["w4_speedup_vs_pp5"] = round(r["pp5"]["ms"] / r["w4"]["ms"], 3)
     res[name] = r
     print(name, json.dumps(r), file=sys.stderr, flush=True)
 os.environ.pop("MTQ_AMD_AWQ_GEMM_MODE", None)
 os.environ.pop("MTQ_AMD_AWQ_PP_PHASES", None)
 os.environ.pop("MTQ_AMD_AWQ_GEMM_PROBE", None)
-os.environ.pop("MTQ_AMD_AWQ_PP_EPI", None)
-os.environ.pop("MTQ_AMD_AWQ_PP_VAR", None)
+os.environ.pop("MTQ_AMD_AWQ_PP_CLAMP", None)
 print(json.dumps({"M": M, "G": G, "rounds": ROUNDS, "shapes": res}))

@@ -86,7 +86,7 @@ def build_sharded(layers: int, device, plan=None):
 
 
 def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", mode="pipeline",
-        algorithm="max", eval_batches=4):
+        algorithm="max", eval_batches=4, baseline=True):
     import modelopt_amd.torch.quantization as mtq
     from modelopt_amd.torch.quantization.sharded import (
         layer_shard_plan,
@@ -114,6 +114,23 @@ def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", m
             for b in batches:
                 m(b)
 
+    def ctx():
+        return layer_sharded_calibration(model, plan) if mode == "pipeline" else contextlib.nullcontext()
+
+    bf16_s = None
+    if baseline:
+        # the same forward passes without quantizers (the model's own bf16 cost of calibration)
+        with ctx():
+            model(batches[0])
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        t0 = time.perf_counter()
+        with ctx():
+            forward_loop(model)
+        torch.cuda.synchronize()
+        bf16_s = _max_over_ranks(time.perf_counter() - t0, dev)
+
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
@@ -121,8 +138,6 @@ def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", m
     # MX presets are dynamic (algorithm None); "max" collects the per-tensor amax anyway so the
     # exported state carries it -- that is the amax the stages exchange
     cfg = {**getattr(mtq, config), "algorithm": None if algorithm == "none" else algorithm}
-    def ctx():
-        return layer_sharded_calibration(model, plan) if mode == "pipeline" else contextlib.nullcontext()
 
     with ctx():
         mtq.quantize(model, cfg, forward_loop)
@@ -148,6 +163,8 @@ def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", m
         "stage_layers": None if plan is None else [plan.first, plan.last],
         "algorithm": algorithm,
         "ptq_wall_clock_s": round(wall, 3), "calib_tokens_per_s": round(samples * seq / wall, 1),
+        "bf16_forward_loop_s": None if bf16_s is None else round(bf16_s, 3),
+        "quantizer_overhead": None if bf16_s is None else round(wall / bf16_s - 1, 4),
         "qdq_forward_tokens_per_s": round(len(ev) * batch * seq * (1 if mode == "pipeline" else world) / qfwd, 1),
         "build_s": round(build_s, 1), "packed_amax_entries": n_amax,
         "hbm_gb_rank0": round(torch.cuda.max_memory_allocated() / 1e9, 1),
@@ -173,14 +190,23 @@ def main():
     ap.add_argument("--mode", choices=["pipeline", "dp"], default="pipeline")
     ap.add_argument("--algorithm", default="max", help='"max" or "none" (the MX preset as is)')
     ap.add_argument("--eval-batches", type=int, default=4)
+    ap.add_argument("--no-baseline", action="store_true")
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="all ranks on cuda:0 (a rehearsal of the N-rank pipeline on a one-GPU box)")
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (ranks sharing one GPU)")
     a = ap.parse_args()
     if "RANK" in os.environ:
-        local = int(os.environ.get("LOCAL_RANK", 0))
+        local = 0 if a.one_gpu else int(os.environ.get("LOCAL_RANK", 0))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(a.backend)
     else:
         torch.cuda.set_device(0)
-    res = run(a.samples, a.seq, a.batch, a.layers, a.config, a.mode, a.algorithm, a.eval_batches)
+    res = run(a.samples, a.seq, a.batch, a.layers, a.config, a.mode, a.algorithm, a.eval_batches,
+              baseline=not a.no_baseline)
+    res["backend"] = dist.get_backend() if dist.is_initialized() else None
     if not dist.is_initialized() or dist.get_rank() == 0:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():

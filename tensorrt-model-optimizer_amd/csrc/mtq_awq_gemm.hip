@@ -370,11 +370,12 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 
 // PROBE (measurement builds only, MTQ_AMD_AWQ_GEMM_PROBE=1): no global loads in the K loop -- the
 // ds_read + MFMA + barrier skeleton alone (the loss is then meaningless)
-// V (A/B of code shapes): bit 0 = transposed MFMA (out^T accumulators, W fragment as the A operand),
-// bit 1 = the last K tile re-loads itself (no branch in the loop) instead of skipping its loads
-template <typename T, bool HAS_BIAS, int PH, int PROBE = 0, int EPI = 0, int V = 1>
+// CLAMP (PH 4): the last K tile re-loads itself (no branch in the loop) instead of skipping its
+// loads (PH 5 always clamps).  Variants measured and dropped in r03 (profiles/r03/awq): two phases
+// per K tile, the untransposed MFMA orientation, reference rows by direct loads, DMA rounds
+// interleaved into the MFMA burst -- none faster than PH 5.
+template <typename T, bool HAS_BIAS, int PH, int PROBE = 0, bool CLAMP = true>
 __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) {
-  constexpr bool TRANS = V & 1, CLAMP = (V >> 1) & 1;
   using namespace pp;
   typedef typename Mfma16<T>::v8 v8;
   __shared__ __attribute__((aligned(16))) unsigned char lds[kLds];
@@ -452,17 +453,89 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (int)(K / kBK);
-  // prologue: K tile 0 in full (A0 B0 B1 A1); phase 0 needs A0 and B0 (PH 4) or A0, B0, B1 (PH 2)
+  // prologue: K tile 0 in full (A0 B0 B1 A1); phase 0 needs A0 and B0
+  if constexpr (PH == 5) {
+    // stream order B0 A0 B1 A1 of tile 0, then B0 A0 of tile 1 (see the PH 5 loop)
+    const int64_t k1 = (int64_t)(nt > 1 ? 1 : 0) * kBK;
+    load_half(1, lds, 0);
+    load_half(0, lds, 0);
+    load_half(2, lds, 0);
+    load_half(3, lds, 0);
+    load_half(1, lds + kBuf, k1);
+    load_half(0, lds + kBuf, k1);
+    wait_vm<8>();
+  } else {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) load_half(q, lds, 0);
-  if constexpr (PH == 4)
+    for (int q = 0; q < 4; ++q) load_half(q, lds, 0);
     wait_vm<4>();
-  else
-    wait_vm<2>();
+  }
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger (wave-uniform: scalar branch)
 
-  if constexpr (PH == 4) {
+  if constexpr (PH == 5) {
+    // Four phases per K tile as PH 4, but the B0 fragments (n-quadrant 0, used by the first and
+    // the last phase) stay in registers from phase 0 to phase 3, so every half-tile's last LDS
+    // read is early: A0 phase 1, B0 phase 0, B1 phase 2, A1 phase 3 (phase 3 reads nothing).
+    // Each half of tile t+2 / t+1 can then be loaded two phases after the same half of tile t /
+    // t-1 was last read (the stagger margin) and still has 4-5 phases to land:
+    //   phase 0: B1(t+1) -> buffer t+1     phase 2: B0(t+2) -> buffer t (B0(t) is in registers)
+    //   phase 1: A1(t+1) -> buffer t+1     phase 3: A0(t+2) -> buffer t (A0(t) read in phase 1)
+    // Waits (before each phase's first barrier, for the next phase's reads): vmcnt(8) -- four
+    // halves issued after the one needed may stay in flight -- and vmcnt(10) in phase 2, whose
+    // successor reads nothing new.
+    v8 af[4][2], b0f[2][2], b1f[2][2];
+    for (int t = 0; t < nt; ++t) {
+      unsigned char *cur = lds + (t & 1) * kBuf;
+      unsigned char *nx1 = lds + ((t + 1) & 1) * kBuf;
+      const int64_t k1 = (int64_t)(t + 1 < nt ? t + 1 : nt - 1) * kBK;  // past the end: harmless re-loads
+      const int64_t k2 = (int64_t)(t + 2 < nt ? t + 2 : nt - 1) * kBK;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int mq = (q == 0 || q == 1) ? 0 : 1;
+        const int nq = (q == 1 || q == 2) ? 1 : 0;
+        if (q == 0 || q == 2) {
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i][s2] = read_a(cur, 4 * mq + i, s2);
+        }
+        if (q == 0) {
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b0f[j][s2] = read_b(cur, j, s2);
+        }
+        if (q == 1) {
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b1f[j][s2] = read_b(cur, 2 + j, s2);
+        }
+        // this phase's half: q0 B1(t+1), q1 A1(t+1) -> buffer t+1; q2 B0(t+2), q3 A0(t+2) -> buffer t
+        const int hq = q == 0 ? 2 : q == 1 ? 3 : q == 2 ? 1 : 0;
+        unsigned char *hb = q < 2 ? nx1 : cur;
+        const int64_t hk = q < 2 ? k1 : k2;
+        if (PROBE == 0) {
+          load_half(hq, hb, hk);
+          if (q == 2)
+            wait_vm<10>();
+          else
+            wait_vm<8>();
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+          const int s2 = kk >> 3, j = (kk >> 2) & 1, i = kk & 3;
+          const v8 bb = nq ? b1f[j][s2] : b0f[j][s2];
+          acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bb, af[i][s2], acc[4 * mq + i][2 * nq + j]);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+  } else {
+    static_assert(PH == 4, "PH 4 or 5");
     v8 af[4][2], bf[2][2];
     for (int t = 0; t < nt; ++t) {
       unsigned char *cur = lds + (t & 1) * kBuf;
@@ -494,76 +567,13 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_setprio(1);
-        if constexpr (TRANS) {
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)  // the A operand (W fragment) held for 4 MFMAs
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bf[j][s], af[i][s], acc[4 * mq + i][2 * nq + j]);
-        } else {
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int j = 0; j < 2; ++j)
-                acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(af[i][s], bf[j][s], acc[4 * mq + i][2 * nq + j]);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
-      }
-    }
-  } else {
-    // PH == 2: two phases per K tile, one m-quadrant (32 MFMAs) each -- half the barriers.
-    // Phase 0 reads the m0 A fragments and ALL B fragments (kept for phase 1) and issues A0, B0,
-    // B1 of the next tile (their last readers were two phases back); phase 1 reads the m1 A
-    // fragments and issues A1.  Waits: after phase 0's six loads, phase 1 needs A1 of this tile
-    // (issued a tile earlier) -> vmcnt(6); after phase 1's two, the next phase needs A0/B0/B1 of
-    // the next tile -> vmcnt(2).
-    v8 af[4][2], bf[4][2];
-    for (int t = 0; t < nt; ++t) {
-      unsigned char *cur = lds + (t & 1) * kBuf;
-      unsigned char *nxt = lds + ((t + 1) & 1) * kBuf;
-      const int64_t kn = (int64_t)(t + 1) * kBK;
-      const bool more = t + 1 < nt;
-#pragma unroll
-      for (int ph = 0; ph < 2; ++ph) {
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) af[i][s] = read_a(cur, 4 * ph + i, s);
-        if (ph == 0) {
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bf[j][s] = read_b(cur, j, s);
-          if (more) {
-            load_half(0, nxt, kn);
-            load_half(1, nxt, kn);
-            load_half(2, nxt, kn);
-            wait_vm<6>();
-          } else {
-            wait_vm<0>();
-          }
-        } else {
-          if (more) {
-            load_half(3, nxt, kn);
-            wait_vm<2>();
-          } else {
-            wait_vm<0>();
-          }
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < 2; ++j)  // the A operand (W fragment) held for 4 MFMAs
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              acc[4 * ph + i][j] = Mfma16<T>::mma(bf[j][s], af[i][s], acc[4 * ph + i][j]);
+              acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bf[j][s], af[i][s], acc[4 * mq + i][2 * nq + j]);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
       }
@@ -572,12 +582,10 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
   if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 
   float sum = 0.f;
-  if constexpr (TRANS) {
   // ---- epilogue.  The MFMAs computed out^T (W fragment as the A operand), so a lane's four
   // accumulators of tile (i, j) are out[m][n .. n+3] with m = 16 i + (lane & 15), n = 16 j +
-  // 4 (lane >> 4): the reference rows come straight from HBM as one 8-byte load each (no LDS
-  // staging, no barrier), all 32 issued before the first use.  Bias, output and difference
-  // rounded to T, fp32 square-sum in a fixed order.
+  // 4 (lane >> 4): one 8-byte LDS read of the staged reference tile each.  Bias, output and
+  // difference rounded to T, fp32 square-sum in a fixed order.
   const T *Y = reinterpret_cast<const T *>(p.yref);
   const T *Bi = reinterpret_cast<const T *>(p.bias);
   typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
@@ -592,15 +600,7 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) rok[i] = m0 + grp * 128 + 16 * i + fr < p.M;
-  if constexpr (EPI == 1) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int64_t r = m0 + grp * 128 + 16 * i + fr;
-      r = rok[i] ? r : p.M - 1;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) yv[i][j] = *reinterpret_cast<const u32x2_t *>(Y + r * p.N + coln[j]);
-    }
-  } else {
+  {
     // the yref tile [256 x 256] through LDS: 16 DMA rounds in flight, row r's 16-byte chunk c
     // stored at chunk c ^ (r & 15) (source-side XOR), so the 16 rows of a b64 read hit 16 slots
     wait_vm<0>();
@@ -651,47 +651,6 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
       }
     }
   }
-  } else {
-    // original orientation: lane holds out[16 i + 4 (lane >> 4) + e][16 j + (lane & 15)]; the
-    // reference tile through LDS (plain [256][256] image) read back per element
-    wait_vm<0>();
-    __syncthreads();
-    const T *Y = reinterpret_cast<const T *>(p.yref);
-    const T *Bi = reinterpret_cast<const T *>(p.bias);
-    {
-      const int ck = tid & 31;
-      int64_t col = n0 + ck * 8;
-      col = col < p.N ? col : p.N - 8;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        int64_t row = m0 + u * 16 + (tid >> 5);
-        row = row < p.M ? row : p.M - 1;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
-                                         (__attribute__((address_space(3))) void *)(lds + u * 8192 + wave * 1024),
-                                         16, 0, 0);
-      }
-    }
-    wait_vm<0>();
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cl = wn * 64 + 16 * j + fr;
-      const bool cok = n0 + cl < p.N;
-      float bj = 0.f;
-      if (HAS_BIAS) bj = Elem<T>::ld(Bi[cok ? n0 + cl : p.N - 1]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rl = grp * 128 + 16 * i + 4 * fq + e;
-          const T yr = *reinterpret_cast<const T *>(lds + rl * 512 + cl * 2);
-          const float y = Elem<T>::ld(Elem<T>::st(acc[i][j][e] + bj));
-          const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr)));
-          sum = (cok && m0 + rl < p.M) ? __builtin_fmaf(d, d, sum) : sum;
-        }
-      }
-    }
-  }
   __syncthreads();
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
@@ -704,6 +663,199 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
     for (int w = 0; w < kThreads / 64; ++w) s += red[w];
     p.partial[(int64_t)g * tiles + tile] = s;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// W4 (mode 2, MTQ_AMD_AWQ_PP_PHASES=6): four waves, ONE wave per SIMD, each wave a 128 x 128 block
+// of the 256 x 256 tile (8 x 8 tiles of 16x16x32, 256 accumulator registers: VGPR + AGPR file of a
+// 512-register wave).  Per K tile (64) a wave reads 32 KiB of fragments (2/3 of the two-group
+// layout's LDS traffic per MFMA) and meets ONE barrier:
+//   phase A: MFMAs of k-step 0 (64) with the k-step 1 fragments of the same tile read beside them;
+//   vmcnt(0) (tile t+1 landed) + lgkmcnt(0), barrier;
+//   phase B: MFMAs of k-step 1 (64) with the k-step 0 fragments of tile t+1 read and tile t+2's
+//            16 LDS-DMA rounds issued into the buffer tile t just vacated.
+// Tile t+2's loads then have phase B of tile t and phase A of tile t+1 (~2k MFMA cycles) to land.
+// Fragments are double-buffered in registers (F0 / F1).  Epilogue as the pp kernel (transposed
+// accumulators, reference rows by 8-byte loads).
+// the accumulators pinned to AGPRs ("+a"): hipcc otherwise shuffles the 256 loop-carried
+// accumulators between the two register files every iteration (v_accvgpr_read/write/mov)
+template <typename T>
+__device__ __forceinline__ void mma_agpr(f32x4 &c, typename Mfma16<T>::v8 a, typename Mfma16<T>::v8 b) {
+  if constexpr (__is_same(T, __bf16))
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+
+template <typename T, bool HAS_BIAS>
+__global__ __launch_bounds__(256, 1) void awq_search_w4_kernel(AwqGemmArgs p) {
+  typedef typename Mfma16<T>::v8 v8;
+  constexpr int kStage = 65536;  // A [256][64] + B [256][64] bf16/f16
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kStage];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, rr8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + orig / 8;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int g = wgid / tiles;
+  const int tile = wgid - g * tiles;
+  constexpr int kGroupM = 8;
+  const int gm = tile / (kGroupM * p.tiles_n);
+  const int first_m = gm * kGroupM;
+  const int gsz = p.tiles_m - first_m < kGroupM ? p.tiles_m - first_m : kGroupM;
+  const int tin = tile - gm * kGroupM * p.tiles_n;
+  const int tm = first_m + tin % gsz, tn = tin / gsz;
+  const int64_t m0 = (int64_t)tm * kBM, n0 = (int64_t)tn * kBN;
+  const int64_t K = p.K;
+  const T *X = reinterpret_cast<const T *>(p.x) + (int64_t)g * p.M * K;
+  const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
+
+  // LDS-DMA: round u (0..7) of an operand writes image bytes [u * 4 KiB + tid * 16): row
+  // u * 32 + (tid >> 3), chunk slot tid & 7 holding source chunk slot ^ ((row >> 1) & 7)
+  unsigned a_off[8], b_off[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int row = u * 32 + (tid >> 3);
+    const int chunk = (tid & 7) ^ ((row >> 1) & 7);
+    int64_t ra = m0 + row;
+    ra = ra < p.M ? ra : p.M - 1;
+    a_off[u] = (unsigned)(ra * K + chunk * 8);
+    int64_t rb = n0 + row;
+    rb = rb < p.N ? rb : p.N - 1;
+    b_off[u] = (unsigned)(rb * K + chunk * 8);
+  }
+  auto dma = [&](const T *base, unsigned off, unsigned char *dst) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(base + off),
+                                     (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+  };
+  auto load_a = [&](unsigned char *stage, int64_t k0, int u) { dma(X + k0, a_off[u], stage + u * 4096 + wave * 1024); };
+  auto load_b = [&](unsigned char *stage, int64_t k0, int u) {
+    dma(W + k0, b_off[u], stage + 32768 + u * 4096 + wave * 1024);
+  };
+  const int sw = (lane >> 1) & 7, fr = lane & 15, fq = lane >> 4;
+  auto read_a = [&](const unsigned char *stage, int i, int s) -> v8 {
+    const int L = wm * 128 + 16 * i + fr;
+    return *reinterpret_cast<const v8 *>(stage + L * 128 + (((4 * s + fq) ^ sw) << 4));
+  };
+  auto read_b = [&](const unsigned char *stage, int j, int s) -> v8 {
+    const int L = wn * 128 + 16 * j + fr;
+    return *reinterpret_cast<const v8 *>(stage + 32768 + L * 128 + (((4 * s + fq) ^ sw) << 4));
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (int)(K / kBK);
+  auto kof = [&](int t) -> int64_t { return (int64_t)(t < nt ? t : nt - 1) * kBK; };
+  // prologue: tiles 0 and 1 (a clamped re-load of tile 0 when K = 64), tile 0's k-step 0 fragments
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { load_a(lds, 0, u); load_b(lds, 0, u); }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { load_a(lds + kStage, kof(1), u); load_b(lds + kStage, kof(1), u); }
+  wait_vm<16>();
+  __syncthreads();
+  // registers: A fragments double-buffered (fa0 / fa1, 64 VGPRs), B fragments rotating in place
+  // (fb[j] is re-read for the next k-step as soon as its 8 MFMAs are issued, 32 VGPRs)
+  v8 fa0[8], fa1[8], fb[8];
+  // the asm MFMAs are opaque to hipcc's hazard padding (cdna_hip_programming.md §5.7 item 2):
+  // wait states between the compiler's accumulator initialisation and the first MFMA here, and
+  // between the last MFMA and the compiler's accumulator reads after the loop
+  asm volatile("s_nop 4" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa0[i] = read_a(lds, i, 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb[j] = read_b(lds, j, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // loop entry with no LDS read pending (as the back-edge)
+
+  for (int t = 0; t < nt; ++t) {
+    unsigned char *cur = lds + (t & 1) * kStage;
+    unsigned char *nxt = lds + ((t + 1) & 1) * kStage;
+    // ---- phase A: k-step 0 of tile t; the k-step 1 fragments of tile t read beside it
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa1[i] = read_a(cur, i, 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mma_agpr<T>(acc[i][j], fb[j], fa0[i]);
+      fb[j] = read_b(cur, j, 1);
+    }
+    wait_vm<0>();  // tile t+1 (this wave's rounds) landed
+    // lgkmcnt(0) through the builtin, which hipcc's wait insertion sees (an asm one it does not,
+    // and it would then wait lgkmcnt(0) again before the first MFMA of the next phase)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase B: k-step 1 of tile t; tile t+1's k-step 0 fragments and tile t+2's DMA
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa0[i] = read_a(nxt, i, 0);
+    const int64_t k2 = kof(t + 2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      // two of tile t+2's sixteen DMA rounds per 8 MFMAs, spread over the phase
+      load_a(cur, k2, j);
+      load_b(cur, k2, j);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mma_agpr<T>(acc[i][j], fb[j], fa1[i]);
+      fb[j] = read_b(nxt, j, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // the next phase A then starts without a wait
+  }
+  wait_vm<0>();
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+  // ---- epilogue: lane holds out[m][n .. n+3], m = wm*128 + 16 i + fr, n = wn*128 + 16 j + 4 fq
+  const T *Y = reinterpret_cast<const T *>(p.yref);
+  const T *Bi = reinterpret_cast<const T *>(p.bias);
+  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+  float sum = 0.f;
+#pragma unroll
+  for (int jh = 0; jh < 2; ++jh) {  // two halves of the columns: 32 reference loads in flight each
+    u32x2_t yv[8][4];
+    bool cok[4];
+    int64_t coln[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int64_t c = n0 + wn * 128 + 16 * (4 * jh + jj) + 4 * fq;
+      cok[jj] = c < p.N;
+      coln[jj] = cok[jj] ? c : p.N - 4;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int64_t r = m0 + wm * 128 + 16 * i + fr;
+      r = r < p.M ? r : p.M - 1;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) yv[i][jj] = *reinterpret_cast<const u32x2_t *>(Y + r * p.N + coln[jj]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool rok = m0 + wm * 128 + 16 * i + fr < p.M;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        T yr[4];
+        __builtin_memcpy(yr, &yv[i][jj], 8);
+        const bool ok = rok && cok[jj];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float bj = HAS_BIAS ? Elem<T>::ld(Bi[coln[jj] + e]) : 0.f;
+          const float y = Elem<T>::ld(Elem<T>::st(acc[i][4 * jh + jj][e] + bj));
+          const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr[e])));
+          sum = ok ? __builtin_fmaf(d, d, sum) : sum;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+  __syncthreads();
+  float *red = reinterpret_cast<float *>(lds);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  if (tid == 0) p.partial[(int64_t)g * tiles + tile] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // xs[g, m, k] = T(x[m, k] * sinv[g, k]) for all g: one read of x, G writes (the reference's
@@ -855,28 +1007,27 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
       awq_search_gemm_kernel<TT, PR, 0><<<grid, kThreads, 0, stream>>>(a);                          \
   } while (0)
   if (mode == 2) {
-    const char *pe = getenv("MTQ_AMD_AWQ_PP_PHASES");  // 4 or 2 phases per K tile (A/B switch)
-    const bool ph2 = pe && atoi(pe) == 2;
-    const char *ee = getenv("MTQ_AMD_AWQ_PP_EPI");  // 0: yref through LDS, 1: direct loads (A/B)
-    const int epi = ee ? atoi(ee) : 0;
-    const char *ve = getenv("MTQ_AMD_AWQ_PP_VAR");  // code-shape variant V (A/B), default 1
-    const int var = ve ? atoi(ve) : 1;
+    // schedule (A/B switch, profiles/r03/awq): 5 = default; 4 = the first r03 schedule (fragments
+    // re-read per phase; MTQ_AMD_AWQ_PP_CLAMP=0 skips the last tile's loads behind a branch);
+    // 6 = W4, one 128 x 128 wave per SIMD
+    const char *pe = getenv("MTQ_AMD_AWQ_PP_PHASES");
+    const int phs = pe ? atoi(pe) : 5;
+    const char *ce = getenv("MTQ_AMD_AWQ_PP_CLAMP");
+    const bool clamp = ce ? atoi(ce) != 0 : true;
 #define MTQ_PP(TT, BB)                                                                              \
   do {                                                                                             \
-    if (ph2)                                                                                       \
-      awq_search_pp_kernel<TT, BB, 2><<<grid, kThreads, 0, stream>>>(a);                            \
-    else if (probe == 1)                                                                           \
+    if (phs == 6)                                                                                  \
+      awq_search_w4_kernel<TT, BB><<<grid, 256, 0, stream>>>(a);                                    \
+    else if (phs == 4 && probe == 1)                                                               \
       awq_search_pp_kernel<TT, BB, 4, 1><<<grid, kThreads, 0, stream>>>(a);                         \
-    else if (epi == 1)                                                                             \
-      awq_search_pp_kernel<TT, BB, 4, 0, 1><<<grid, kThreads, 0, stream>>>(a);                      \
-    else if (var == 0)                                                                             \
-      awq_search_pp_kernel<TT, BB, 4, 0, 0, 0><<<grid, kThreads, 0, stream>>>(a);                   \
-    else if (var == 2)                                                                             \
-      awq_search_pp_kernel<TT, BB, 4, 0, 0, 2><<<grid, kThreads, 0, stream>>>(a);                   \
-    else if (var == 3)                                                                             \
-      awq_search_pp_kernel<TT, BB, 4, 0, 0, 3><<<grid, kThreads, 0, stream>>>(a);                   \
-    else                                                                                           \
+    else if (phs == 4 && !clamp)                                                                   \
+      awq_search_pp_kernel<TT, BB, 4, 0, false><<<grid, kThreads, 0, stream>>>(a);                  \
+    else if (phs == 4)                                                                             \
       awq_search_pp_kernel<TT, BB, 4><<<grid, kThreads, 0, stream>>>(a);                            \
+    else if (probe == 1)                                                                           \
+      awq_search_pp_kernel<TT, BB, 5, 1><<<grid, kThreads, 0, stream>>>(a);                         \
+    else                                                                                           \
+      awq_search_pp_kernel<TT, BB, 5><<<grid, kThreads, 0, stream>>>(a);                            \
   } while (0)
     if (dtype == MTQ_BF16) {
       if (bias)
