@@ -193,6 +193,33 @@ int mtq_qlinear_small_m_ws(const void *x, const void *w, const void *bias, void 
                            int is_unsigned, int narrow_range, void *ws, size_t ws_bytes,
                            hipStream_t stream);
 
+/* Up to 4 short-input linears of the same M and K in ONE launch (the q/k/v projections of a decode
+ * step, each reading the same hidden state through its own input quantizer): problem i computes
+ * y_i[M, N_i] = x_i . qdq_i(W_i)^T (+ bias_i) exactly as mtq_qlinear_small_m_ws would (same qdq,
+ * same per-linear split-K chunk order for a given split), the units of all linears sharing one
+ * grid.  Linears that cannot share a launch (different `kind` or amax class, non-fp32 amax, blocks
+ * not aligned to the stream kernel's batches) run one after another.  Reference: the separate
+ * k_proj / v_proj (q_proj) forwards of an HF attention module, each the QuantLinear forward of
+ * nn/modules/quant_module.py:257-278.  `ws`: mtq_qlinear_small_m_group_workspace_bytes bytes. */
+typedef struct {
+  const void *x;
+  const void *w;
+  const void *bias;
+  void *y;
+  int64_t N;
+  const void *amax;
+  int amax_dtype;
+  int64_t amax_numel;
+  int64_t block;
+  int kind;
+  int num_bits;
+  int is_unsigned;
+  int narrow_range;
+} mtq_qlinear_problem;
+size_t mtq_qlinear_small_m_group_workspace_bytes(int64_t M, const int64_t *N, int n, int64_t K);
+int mtq_qlinear_small_m_group(const mtq_qlinear_problem *problems, int n, int64_t M, int64_t K,
+                              int dtype, void *ws, size_t ws_bytes, hipStream_t stream);
+
 /* ---- checkpoint export (real-quant packing) ----------------------------------------------
  * export/quant_utils.py:836-938 to_quantized_weight and the qtensor quantize() routines; weights
  * [rows, cols] row-major of dtype, outputs raw bytes.

@@ -6,6 +6,8 @@ gate/up 14336x4096, down 4096x14336: 218 M weights, 436 MB bf16 -- larger than t
 Infinity Cache, so every pass streams W from HBM) at M = 1 / 4 / 16 input rows:
 
   fused    ops.qlinear_small_m: weight fake quant applied to the MFMA operands (one pass over W)
+  grouped  the same, with q/k/v_proj as ONE ops.qlinear_small_m_group launch (what the HF
+           attention wrapper runs for a decode step) and the other four linears as above
   unfused  the reference's QuantLinear forward: W_q = qdq(W) (read W, write W_q), then
            F.linear(x, W_q) on hipBLASLt (read W_q)
   bf16     F.linear(x, W) without quantization (hipBLASLt), the floor for any simulated GEMM
@@ -121,11 +123,34 @@ def main():
                         wq = ops.quantize_op(w.view(-1, b), am, nb, 4 if kind else 0, False, False).view_as(w)
                     F.linear(xs[w.shape[1]], wq)
 
-            t_f, t_u = timed(fused, a.iters), timed(unfused, a.iters)
+            def grouped():
+                x = xs[4096]
+                ops.qlinear_small_m_group([x, x, x], ws[:3], [None] * 3, amaxs[:3], blocks[:3], kind, [nb] * 3,
+                                          [0] * 3, [0] * 3)
+                for w, am, b in zip(ws[3:], amaxs[3:], blocks[3:]):
+                    ops.qlinear_small_m(xs[w.shape[1]], w, None, am, b, kind, nb, False, False)
+
+            def qkv_grouped():
+                x = xs[4096]
+                ops.qlinear_small_m_group([x, x, x], ws[:3], [None] * 3, amaxs[:3], blocks[:3], kind, [nb] * 3,
+                                          [0] * 3, [0] * 3)
+
+            def qkv_single():
+                for w, am, b in zip(ws[:3], amaxs[:3], blocks[:3]):
+                    ops.qlinear_small_m(xs[4096], w, None, am, b, kind, nb, False, False)
+
+            t_f, t_u, t_g = timed(fused, a.iters), timed(unfused, a.iters), timed(grouped, a.iters)
+            t_qg, t_qs = timed(qkv_grouped, a.iters), timed(qkv_single, a.iters)
             gbs = wbytes / (t_f * 1e-3) / 1e9
+            gbg = wbytes / (t_g * 1e-3) / 1e9
+            qkv_bytes = sum(w.numel() * 2 for w in ws[:3])
             res["results"][f"M={m}"][name] = {
                 "fused_ms": round(t_f, 4), "unfused_ms": round(t_u, 4), "speedup": round(t_u / t_f, 2),
                 "fused_weight_GB_s": round(gbs, 1), "fused_frac_hbm": round(gbs / 8000.0, 4),
+                "grouped_qkv_layer_ms": round(t_g, 4), "grouped_weight_GB_s": round(gbg, 1),
+                "grouped_frac_hbm": round(gbg / 8000.0, 4),
+                "qkv_grouped_us": round(t_qg * 1e3, 2), "qkv_three_launches_us": round(t_qs * 1e3, 2),
+                "qkv_grouped_GB_s": round(qkv_bytes / (t_qg * 1e-3) / 1e9, 1),
             }
         # per-linear split of the fused INT4 path (launch / latency-bound small matrices)
         for name in ("int4_block128 (INT4_AWQ weights)", "fp8_per_tensor (FP8_DEFAULT weights)"):

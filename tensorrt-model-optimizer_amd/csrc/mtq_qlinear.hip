@@ -336,19 +336,18 @@ template <int XM> struct XLayout {
 
 // PROBE (measurement builds): 1 = raw W to the MFMA, 2 = no qdq and no MFMA (the slot's bits
 // folded into the accumulator); RING overrides the ring depth (0: XLayout's)
+// One unit (16-row tile x K chunk) of one linear; `unit` and `wave` wave-uniform.
 template <typename T, int KIND, bool PT, int XM, int PROBE = 0, int RING = 0>
-__global__ __launch_bounds__(kStreamWaves * 64) void qlinear_dma_kernel(
+__device__ __forceinline__ void qlinear_dma_unit(
     const T *__restrict__ x, const T *__restrict__ w, T *__restrict__ y, const T *__restrict__ bias,
-    float *__restrict__ part, int M, int N, int K, int tiles, int S, int kcs, QlParams p) {
+    float *__restrict__ part, int M, int N, int K, int tiles, int S, int kcs, const QlParams &p,
+    int unit, int wave) {
   constexpr int U = 4;
   using XL = XLayout<XM>;
   constexpr int R = RING ? RING : XL::ring, SLOT = XL::slot;
   constexpr int GROUP = 4 + XL::dmas + (PT ? 0 : 1);  // DMA instructions per batch
   __shared__ __attribute__((aligned(16))) unsigned char lds[kStreamWaves * R * SLOT];
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * kStreamWaves) + wave;
-  if (unit >= tiles * S) return;  // wave-uniform; the kernel has no barrier
   const int tile = unit % tiles, chunk = unit / tiles;
   const int r = lane & 15, qd = lane >> 4;
   const int nsteps = K >> 5;
@@ -499,6 +498,47 @@ __global__ __launch_bounds__(kStreamWaves * 64) void qlinear_dma_kernel(
   }
 }
 
+template <typename T, int KIND, bool PT, int XM, int PROBE = 0, int RING = 0>
+__global__ __launch_bounds__(kStreamWaves * 64) void qlinear_dma_kernel(
+    const T *__restrict__ x, const T *__restrict__ w, T *__restrict__ y, const T *__restrict__ bias,
+    float *__restrict__ part, int M, int N, int K, int tiles, int S, int kcs, QlParams p) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * kStreamWaves) + wave;
+  if (unit >= tiles * S) return;  // wave-uniform; the kernel has no barrier
+  qlinear_dma_unit<T, KIND, PT, XM, PROBE, RING>(x, w, y, bias, part, M, N, K, tiles, S, kcs, p, unit, wave);
+}
+
+// Several linears of the same input length M and depth K in one launch (the q/k/v projections of
+// a decode step: 8 MB k/v weight streams alone cannot fill the chip or amortise a launch).  The
+// units of linear i are [uend[i-1], uend[i]); every linear splits K the same way (S, kcs).
+constexpr int kMaxGroup = 4;
+struct QlGroupArgs {
+  const void *x[kMaxGroup], *w[kMaxGroup], *bias[kMaxGroup];
+  void *y[kMaxGroup];
+  float *part[kMaxGroup];
+  int N[kMaxGroup], uend[kMaxGroup];
+  QlParams p[kMaxGroup];
+  int n, M, K, S, kcs;
+};
+
+template <typename T, int KIND, bool PT, int XM>
+__global__ __launch_bounds__(kStreamWaves * 64) void qlinear_dma_group_kernel(QlGroupArgs g) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * kStreamWaves) + wave;
+  if (unit >= g.uend[g.n - 1]) return;  // wave-uniform
+  int i = 0, base = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxGroup - 1; ++j)
+    if (j < g.n - 1 && unit >= g.uend[j]) {
+      i = j + 1;
+      base = g.uend[j];
+    }
+  const int N = g.N[i];
+  qlinear_dma_unit<T, KIND, PT, XM>(reinterpret_cast<const T *>(g.x[i]), reinterpret_cast<const T *>(g.w[i]),
+                                    reinterpret_cast<T *>(g.y[i]), reinterpret_cast<const T *>(g.bias[i]),
+                                    g.part[i], g.M, N, g.K, N / 16, g.S, g.kcs, g.p[i], unit - base, wave);
+}
+
 // y[m, n] = sum over chunks in order of part[c, m, n] (+ bias[n]), one rounding
 template <typename T>
 __global__ __launch_bounds__(256) void qlinear_splitk_finish(const float *__restrict__ part,
@@ -520,6 +560,34 @@ __global__ __launch_bounds__(256) void qlinear_splitk_finish(const float *__rest
   for (; c < S; ++c) v += part[(int64_t)c * MN + i];
   if (bias) v += Elem<T>::ld(bias[i % N]);
   y[i] = Elem<T>::st(v);
+}
+
+struct QlFinishGroupArgs {
+  const float *part[kMaxGroup];
+  const void *bias[kMaxGroup];
+  void *y[kMaxGroup];
+  int N[kMaxGroup], mnend[kMaxGroup];
+  int n, M, S;
+};
+// the split-K finish of every linear of a group in one launch (same fixed chunk order)
+template <typename T>
+__global__ __launch_bounds__(256) void qlinear_splitk_finish_group(QlFinishGroupArgs a) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= a.mnend[a.n - 1]) return;
+  int k = 0, base = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxGroup - 1; ++j)
+    if (j < a.n - 1 && t >= a.mnend[j]) {
+      k = j + 1;
+      base = a.mnend[j];
+    }
+  const int i = t - base, MN = a.M * a.N[k];
+  const float *part = a.part[k];
+  float v = 0.f;
+  for (int c = 0; c < a.S; ++c) v += part[(int64_t)c * MN + i];
+  const T *bias = reinterpret_cast<const T *>(a.bias[k]);
+  if (bias) v += Elem<T>::ld(bias[i % a.N[k]]);
+  reinterpret_cast<T *>(a.y[k])[i] = Elem<T>::st(v);
 }
 
 // ---- workgroup-per-tile kernel (blocks not aligned to the stream kernel's batches) ----------
@@ -813,4 +881,135 @@ extern "C" int mtq_qlinear_small_m(const void *x, const void *w, const void *bia
                                    hipStream_t stream) {
   return mtq_qlinear_small_m_ws(x, w, bias, y, M, N, K, dtype, amax, amax_dtype, amax_numel, block,
                                 kind, num_bits, is_unsigned, narrow_range, nullptr, 0, stream);
+}
+
+namespace {
+
+// the problems run as one grouped launch: same kind, fp32 amax of one class (per tensor, or
+// per-row blocks aligned to the 128-column batches), the LDS-DMA kernel not switched off
+bool groupable(const mtq_qlinear_problem *pr, int n, int64_t K) {
+  if (n < 1 || n > kMaxGroup || force_wg() || env_int("MTQ_AMD_QLINEAR_VARIANT", 0) != 0 ||
+      env_int("MTQ_AMD_QLINEAR_PROBE", 0) != 0)
+    return false;
+  const bool pt = pr[0].amax_numel == 1;
+  for (int i = 0; i < n; ++i) {
+    if (pr[i].kind != pr[0].kind || pr[i].amax_dtype != 0 || (pr[i].amax_numel == 1) != pt) return false;
+    if (!pt && stream_spb(pr[i].amax_numel, pr[i].block, K) != 0) return false;
+  }
+  return true;
+}
+
+int64_t group_part_floats(const mtq_qlinear_problem *pr, int n, int64_t M, const Split &sp) {
+  int64_t f = 0;
+  for (int i = 0; i < n; ++i) f += sp.S > 1 ? (int64_t)sp.S * M * pr[i].N : 0;
+  return f;
+}
+
+Split group_split(const int64_t *N, int n, int64_t K) {
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) total += N[i];
+  return choose_split(total, K, true);
+}
+
+template <typename T, int KIND, bool PT, int XM>
+void launch_group(const QlGroupArgs &g, unsigned grid, hipStream_t stream) {
+  qlinear_dma_group_kernel<T, KIND, PT, XM><<<grid, kStreamWaves * 64, 0, stream>>>(g);
+}
+
+template <typename T, int KIND>
+int run_group(const mtq_qlinear_problem *pr, int n, int64_t M, int64_t K, float *ws, Split sp,
+              hipStream_t stream) {
+  QlGroupArgs g{};
+  g.n = n, g.M = (int)M, g.K = (int)K, g.S = sp.S, g.kcs = sp.kcs;
+  QlFinishGroupArgs f{};
+  f.n = n, f.M = (int)M, f.S = sp.S;
+  int units = 0, mn = 0;
+  int64_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    g.x[i] = pr[i].x, g.w[i] = pr[i].w, g.bias[i] = pr[i].bias, g.y[i] = pr[i].y;
+    g.N[i] = (int)pr[i].N;
+    g.part[i] = sp.S > 1 ? ws + off : nullptr;
+    off += sp.S > 1 ? (int64_t)sp.S * M * pr[i].N : 0;
+    QlParams &p = g.p[i];
+    p = QlParams{pr[i].amax, pr[i].amax_dtype, pr[i].amax_numel, pr[i].block, 0.f, 0.f};
+    if (KIND == 0) {
+      const float mb = (float)((1ll << (pr[i].num_bits - 1 + (pr[i].is_unsigned ? 1 : 0))) - 1);
+      p.max_bound = mb;
+      p.min_bound = pr[i].is_unsigned ? 0.f : (pr[i].narrow_range ? -mb : -mb - 1.f);
+    }
+    units += (int)(pr[i].N / 16) * sp.S;
+    g.uend[i] = units;
+    f.part[i] = g.part[i], f.bias[i] = pr[i].bias, f.y[i] = pr[i].y, f.N[i] = (int)pr[i].N;
+    mn += (int)(M * pr[i].N);
+    f.mnend[i] = mn;
+  }
+  const unsigned grid = (unsigned)((units + kStreamWaves - 1) / kStreamWaves);
+  const bool pt = pr[0].amax_numel == 1;
+#define QL_GROUP(XM)                                         \
+  do {                                                       \
+    if (pt)                                                  \
+      launch_group<T, KIND, true, XM>(g, grid, stream);      \
+    else                                                     \
+      launch_group<T, KIND, false, XM>(g, grid, stream);     \
+  } while (0)
+  if (M == 1)
+    QL_GROUP(1);
+  else if (M <= 4)
+    QL_GROUP(4);
+  else if (M <= 8)
+    QL_GROUP(8);
+  else
+    QL_GROUP(16);
+#undef QL_GROUP
+  int st = host_check_launch();
+  if (st != MTQ_OK || sp.S == 1) return st;
+  qlinear_splitk_finish_group<T><<<(unsigned)((mn + 255) / 256), 256, 0, stream>>>(f);
+  return host_check_launch();
+}
+
+}  // namespace
+
+extern "C" size_t mtq_qlinear_small_m_group_workspace_bytes(int64_t M, const int64_t *N, int n, int64_t K) {
+  if (M < 1 || K < 32 || !N || n < 1 || n > kMaxGroup) return 0;
+  int64_t Ns[kMaxGroup];
+  size_t single = 0;
+  for (int i = 0; i < n; ++i) {
+    if (N[i] < 16) return 0;
+    Ns[i] = N[i];
+    const size_t b = mtq_qlinear_small_m_workspace_bytes(M, N[i], K);
+    single = b > single ? b : single;  // the fallback runs the linears one after another
+  }
+  const Split sp = group_split(Ns, n, K);
+  int64_t f = 0;
+  for (int i = 0; i < n; ++i) f += sp.S > 1 ? (int64_t)sp.S * M * Ns[i] : 0;
+  const size_t grouped = (size_t)f * sizeof(float);
+  return grouped > single ? grouped : single;
+}
+
+extern "C" int mtq_qlinear_small_m_group(const mtq_qlinear_problem *pr, int n, int64_t M, int64_t K,
+                                         int dtype, void *ws, size_t ws_bytes, hipStream_t stream) {
+  if (!pr || n < 1 || n > kMaxGroup) return MTQ_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i) {
+    const int st = validate(pr[i].x, pr[i].w, pr[i].y, M, pr[i].N, K, dtype, pr[i].amax, pr[i].amax_dtype,
+                            pr[i].amax_numel, pr[i].block, pr[i].kind, pr[i].num_bits);
+    if (st != MTQ_OK) return st;
+  }
+  int64_t Ns[kMaxGroup];
+  for (int i = 0; i < n; ++i) Ns[i] = pr[i].N;
+  Split sp = group_split(Ns, n, K);
+  if (groupable(pr, n, K) && (sp.S == 1 || (ws && al16(ws) && ws_bytes >= (size_t)group_part_floats(pr, n, M, sp) * sizeof(float)))) {
+    float *part = reinterpret_cast<float *>(ws);
+    const bool bf = dtype == MTQ_BF16, k0 = pr[0].kind == 0;
+    if (bf) return k0 ? run_group<__bf16, 0>(pr, n, M, K, part, sp, stream) : run_group<__bf16, 1>(pr, n, M, K, part, sp, stream);
+    return k0 ? run_group<_Float16, 0>(pr, n, M, K, part, sp, stream) : run_group<_Float16, 1>(pr, n, M, K, part, sp, stream);
+  }
+  // not groupable: one launch per linear, in order (same results as separate calls)
+  for (int i = 0; i < n; ++i) {
+    const int st = mtq_qlinear_small_m_ws(pr[i].x, pr[i].w, pr[i].bias, pr[i].y, M, pr[i].N, K, dtype, pr[i].amax,
+                                          pr[i].amax_dtype, pr[i].amax_numel, pr[i].block, pr[i].kind,
+                                          pr[i].num_bits, pr[i].is_unsigned, pr[i].narrow_range, ws, ws_bytes,
+                                          stream);
+    if (st != MTQ_OK) return st;
+  }
+  return MTQ_OK;
 }

@@ -797,6 +797,64 @@ at::Tensor qlinear_small_m(const at::Tensor &input, const at::Tensor &weight,
   return y;
 }
 
+// Up to 4 short-input linears of one M and K in one launch (mtq_qlinear_small_m_group): the
+// q/k/v projections of a decode step.  Per linear as qlinear_small_m; flags as 0/1 ints.
+std::vector<at::Tensor> qlinear_small_m_group(at::TensorList inputs, at::TensorList weights,
+                                              const c10::List<c10::optional<at::Tensor>> &biases,
+                                              at::TensorList amaxs, at::IntArrayRef blocks, int64_t kind,
+                                              at::IntArrayRef num_bits, at::IntArrayRef is_unsigned,
+                                              at::IntArrayRef narrow_range) {
+  const size_t n = inputs.size();
+  TORCH_CHECK(n >= 1 && n <= 4, "qlinear_small_m_group: 1 to 4 linears");
+  TORCH_CHECK(weights.size() == n && biases.size() == n && amaxs.size() == n && blocks.size() == n &&
+                  num_bits.size() == n && is_unsigned.size() == n && narrow_range.size() == n,
+              "qlinear_small_m_group: one entry per linear in every list");
+  check_device(inputs[0], "input");
+  const int dt = checked_dtype(inputs[0], "input");
+  const int64_t K = inputs[0].size(-1);
+  const int64_t M = K ? inputs[0].numel() / K : 0;
+  std::vector<at::Tensor> xs, ws, as, bs, ys;
+  std::vector<mtq_qlinear_problem> pr(n);
+  std::vector<int64_t> Ns(n);
+  for (size_t i = 0; i < n; ++i) {
+    check_device(inputs[i], "input");
+    check_device(weights[i], "weight");
+    TORCH_CHECK(weights[i].dim() == 2 && weights[i].size(1) == K && inputs[i].size(-1) == K &&
+                    inputs[i].numel() == M * K,
+                "qlinear_small_m_group: every linear needs the same input rows and K");
+    TORCH_CHECK(inputs[i].scalar_type() == inputs[0].scalar_type() &&
+                    weights[i].scalar_type() == inputs[0].scalar_type(),
+                "qlinear_small_m_group: one dtype for all inputs and weights");
+    xs.push_back(inputs[i].contiguous());
+    ws.push_back(weights[i].contiguous());
+    as.push_back(amaxs[i].to(at::kFloat).contiguous());
+    TORCH_CHECK(as.back().device() == xs.back().device(), "qlinear_small_m_group: amax device");
+    at::Tensor b;
+    const c10::optional<at::Tensor> bo = biases.get(i);
+    if (bo.has_value() && bo->defined()) {
+      b = bo->contiguous();
+      TORCH_CHECK(b.scalar_type() == xs.back().scalar_type() && b.numel() == weights[i].size(0),
+                  "qlinear_small_m_group: bias");
+    }
+    bs.push_back(b);
+    std::vector<int64_t> shape(inputs[i].sizes().begin(), inputs[i].sizes().end());
+    shape.back() = weights[i].size(0);
+    ys.push_back(at::empty(shape, xs.back().options()));
+    Ns[i] = weights[i].size(0);
+    pr[i] = mtq_qlinear_problem{xs[i].data_ptr(), ws[i].data_ptr(), b.defined() ? b.data_ptr() : nullptr,
+                                ys[i].data_ptr(), Ns[i], as[i].data_ptr(), checked_dtype(as[i], "amax"),
+                                as[i].numel(), blocks[i], (int)kind, (int)num_bits[i], (int)is_unsigned[i],
+                                (int)narrow_range[i]};
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(xs[0].device());
+  const size_t wsb = M >= 1 && M <= 16 ? mtq_qlinear_small_m_group_workspace_bytes(M, Ns.data(), (int)n, K) : 0;
+  at::Tensor wsp = at::empty({(int64_t)(wsb / sizeof(float))}, xs[0].options().dtype(at::kFloat));
+  check_status(mtq_qlinear_small_m_group(pr.data(), (int)n, M, K, dt, wsb ? wsp.data_ptr() : nullptr, wsb,
+                                         cur_stream(xs[0])),
+               "qlinear_small_m_group");
+  return ys;
+}
+
 void histogram_abs_accumulate(const at::Tensor &inputs, const at::Tensor &hmax, at::Tensor counts,
                               int64_t bins, bool skip_zeros) {
   at::Tensor x = inputs.contiguous();
@@ -942,6 +1000,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "bool unsigned, bool narrow_range) -> Tensor");
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
         "bool skip_zeros) -> ()");
+  m.def("qlinear_small_m_group(Tensor[] inputs, Tensor[] weights, Tensor?[] biases, Tensor[] amaxs, int[] blocks, "
+        "int kind, int[] num_bits, int[] is_unsigned, int[] narrow_range) -> Tensor[]");
   m.def("qlinear_small_m(Tensor input, Tensor weight, Tensor? bias, Tensor amax, int block, int kind, "
         "int num_bits, bool unsigned, bool narrow_range) -> Tensor");
   m.def("mse_accumulate(Tensor a, Tensor b, Tensor(a!) loss, int index) -> ()");
@@ -972,6 +1032,7 @@ TORCH_LIBRARY(modelopt_amd, m) {
 TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("quantize_op", &quantize_op);
   m.impl("qlinear_small_m", &qlinear_small_m);
+  m.impl("qlinear_small_m_group", &qlinear_small_m_group);
   m.impl("dynamic_block_quantize_op", &dynamic_block_quantize_op);
   m.impl("fake_tensor_quant", &fake_tensor_quant);
   m.impl("fake_tensor_quant_", &fake_tensor_quant_);

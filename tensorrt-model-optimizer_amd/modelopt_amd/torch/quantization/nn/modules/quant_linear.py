@@ -60,8 +60,9 @@ def _fused_weight_params(wq, weight):
     return None
 
 
-def _fused_forward(mod, input):
-    """The fused short-input forward, or None when the module/input does not qualify."""
+def _fused_params(mod, input):
+    """(weight, bias, (amax, block, kind)) when ``mod`` can run the fused short-input forward on
+    ``input``; None otherwise.  No side effects (the input quantizer is not applied)."""
     if not _FUSED[0] or input.device.type != "cuda" or input.dtype not in (torch.bfloat16, torch.float16):
         return None
     weight = mod._parameters.get("weight")
@@ -80,20 +81,87 @@ def _fused_forward(mod, input):
     p = _fused_weight_params(wq, weight)
     if p is None:
         return None
-    amax, block, kind = p
     bias = mod._parameters.get("bias")
     if bias is not None and bias.dtype != input.dtype:
         return None
+    return weight, bias, p
+
+
+def _fused_input(mod, input):
     x = mod.input_quantizer(input)
     if x.dtype != input.dtype:
         return None
     x = x.contiguous()
     if x.data_ptr() % 16:
         x = x.clone()  # the MFMA operand loads are 16-byte vectors
+    return x
+
+
+def _fused_forward(mod, input):
+    """The fused short-input forward, or None when the module/input does not qualify."""
+    fp = _fused_params(mod, input)
+    if fp is None:
+        return None
+    weight, bias, (amax, block, kind) = fp
+    x = _fused_input(mod, input)
+    if x is None:
+        return None
+    wq = mod._modules["weight_quantizer"]
     return _ops().qlinear_small_m(
         x, weight, bias, amax, block, kind, wq._num_bits if kind == 0 else 8, bool(wq._unsigned),
         bool(wq._narrow_range),
     )
+
+
+class ProjectionGroup:
+    """The projections of one attention forward that read the same hidden state (q/k/v_proj):
+    the first of them to be called with a short input runs all of them as ONE launch
+    (``qlinear_small_m_group``) and hands the others their outputs when they are called with the
+    same tensor.  Each input quantizer is still applied exactly once, each output is what that
+    projection's own fused forward computes (only the split-K chunking may differ); if any member
+    does not qualify, every member takes its own path.  Installed by the HF attention wrapper for
+    the duration of one forward (plugins/huggingface.py ``_QuantAttention``)."""
+
+    def __init__(self, mods):
+        self.mods = list(mods)
+        self.tried = False
+        self.key = None
+        self.outs = {}
+
+    def take(self, mod, input):
+        if self.key is not None:
+            if input is self.key[0] and input._version == self.key[1]:
+                return self.outs.pop(id(mod), None)
+            return None
+        if self.tried:
+            return None
+        self.tried = True  # one attempt per forward
+        params = [_fused_params(m, input) for m in self.mods]
+        if any(p is None for p in params) or len({p[2][2] for p in params}) != 1:
+            return None
+        xs = [_fused_input(m, input) for m in self.mods]
+        if any(x is None for x in xs):
+            # an input quantizer changed the dtype (as in _fused_forward, that member then takes
+            # the reference path); the others finish on their own operands
+            outs = [None if x is None else self._single(m, x, p) for m, x, p in zip(self.mods, xs, params)]
+        else:
+            wqs = [m._modules["weight_quantizer"] for m in self.mods]
+            kind = params[0][2][2]
+            outs = _ops().qlinear_small_m_group(
+                xs, [p[0] for p in params], [p[1] for p in params], [p[2][0] for p in params],
+                [p[2][1] for p in params], kind, [q._num_bits if kind == 0 else 8 for q in wqs],
+                [int(bool(q._unsigned)) for q in wqs], [int(bool(q._narrow_range)) for q in wqs],
+            )
+        self.key = (input, input._version)
+        self.outs = {id(m): y for m, y in zip(self.mods, outs) if m is not mod and y is not None}
+        return outs[self.mods.index(mod)]
+
+    @staticmethod
+    def _single(m, x, p):
+        weight, bias, (amax, block, kind) = p
+        wq = m._modules["weight_quantizer"]
+        return _ops().qlinear_small_m(x, weight, bias, amax, block, kind, wq._num_bits if kind == 0 else 8,
+                                      bool(wq._unsigned), bool(wq._narrow_range))
 
 
 @QuantModuleRegistry.register({nn.Linear: "nn.Linear"})
@@ -104,6 +172,11 @@ class _QuantLinear(QuantLinearConvBase):
 
     def forward(self, input, *args, **kwargs):
         if not args and not kwargs:
+            group = self.__dict__.get("_projection_group")
+            if group is not None:
+                y = group.take(self, input)
+                if y is not None:
+                    return y
             y = _fused_forward(self, input)
             if y is not None:
                 return y

@@ -17,6 +17,7 @@ import inspect
 import torch
 import torch.nn as nn
 
+from ..nn.modules import quant_linear as _quant_linear
 from ..nn.modules.quant_module import QuantModule, QuantModuleRegistry
 from ..nn.modules.tensor_quantizer import TensorQuantizer
 from . import register_on_the_fly
@@ -74,15 +75,19 @@ class _QuantFusedExperts(QuantModule):
         # is routed to some expert and the shared input quantizer acts on each token on its own,
         # applying it ONCE to hidden_states (collect and/or fake quant) equals applying it to each
         # expert's gather -- max over the union = max of the per-expert maxima, and a per-element
-        # qdq commutes with the gather -- so one reduction / qdq launch replaces E of them.
+        # qdq commutes with the gather -- so one reduction / qdq launch replaces E of them.  Rows
+        # routed to no local expert (index outside [0, E): expert-parallel sentinels) are zeroed
+        # first, on the device (no host sync): |0| adds nothing to a running max, and no expert
+        # gathers those rows.
         args = list(args)
         hs = args[0] if args else kwargs.get("hidden_states")
         idx_t = args[1] if len(args) > 1 else kwargs.get("top_k_index")
         if (
             isinstance(hs, torch.Tensor) and hs.dim() == 2 and isinstance(idx_t, torch.Tensor)
-            and _token_separable(first_in) and bool((idx_t < self.num_experts).all())
+            and idx_t.dim() == 2 and idx_t.shape[0] == hs.shape[0] and _token_separable(first_in)
         ):
-            hs = first_in(hs)
+            routed = ((idx_t >= 0) & (idx_t < self.num_experts)).any(dim=-1, keepdim=True)
+            hs = first_in(torch.where(routed, hs, hs.new_zeros(())))
             if args:
                 args[0] = hs
             else:
@@ -456,15 +461,33 @@ class _QuantAttention(QuantModule):
             module.eager_attention_forward = patch_fn
         else:
             registry[impl] = patch_fn
+        # decode-shaped steps: the q/k/v projections (same hidden state) as one fused launch
+        projs = self._qkv_projections()
+        if projs:
+            group = _quant_linear.ProjectionGroup(projs)
+            for m in projs:
+                m.__dict__["_projection_group"] = group
         try:
             return self._original_cls.forward(self, *args, **kwargs)
         finally:
+            for m in projs:
+                m.__dict__.pop("_projection_group", None)
             if eager:
                 module.eager_attention_forward = original
             elif had_local:
                 registry[impl] = original
             else:
                 del registry[impl]
+
+    def _qkv_projections(self) -> list:
+        """q_proj / k_proj / v_proj when they are separate quantized linears (MI355X addition:
+        decode steps run them as one grouped launch, see ``ProjectionGroup``)."""
+        if not _quant_linear._FUSED[0]:
+            return []
+        mods = [self._modules.get(n) for n in ("q_proj", "k_proj", "v_proj")]
+        if any(not isinstance(m, _quant_linear._QuantLinear) for m in mods):
+            return []
+        return mods
 
 
 def _wraps_nested_attention(module) -> bool:

@@ -172,3 +172,91 @@ def test_quant_linear_long_inputs_and_grad_use_reference_path(gpu):
     assert ql._fused_forward(model, x) is None
     model(x).sum().backward()
     assert x.grad is not None
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("m", [1, 5, 16])
+@pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[4], CASES[5]])
+def test_group_launch_against_fp64(gpu, dtype, m, case):
+    """q/k/v-shaped linears (different N, same K and input rows) in one grouped launch: each
+    output within the single kernel's fp32-accumulation bound of its own fp64 product, bias on one
+    of them, per-linear amax (and for INT-n per-linear num_bits flags)."""
+    kind, nb, uns, narrow, layout = case
+    k = 1024
+    g = torch.Generator().manual_seed(m + 11 * kind)
+    ns = [256, 64, 64]
+    ws = [(torch.randn(n, k, generator=g) * 0.05).to(dtype) for n in ns]
+    xs = [torch.randn(m, k, generator=g).to(dtype) for _ in ns]
+    bs = [None, (torch.randn(64, generator=g) * 0.1).to(dtype), None]
+    am = [make_amax(w, layout) for w in ws]
+    ys = ops().qlinear_small_m_group([x.to(gpu) for x in xs], [w.to(gpu) for w in ws],
+                                     [None if b is None else b.to(gpu) for b in bs], [a.to(gpu) for a, _ in am],
+                                     [blk for _, blk in am], kind, [nb] * 3, [int(uns)] * 3, [int(narrow)] * 3)
+    ulp = 2.0 ** -7 if dtype == torch.bfloat16 else 2.0 ** -10
+    for x, w, b, (a, blk), y in zip(xs, ws, bs, am, ys):
+        wq = oracle_wq(w, a, blk, kind, nb, uns, narrow)
+        exact = x.double() @ wq.double().t() + (0 if b is None else b.double())
+        mag = x.double().abs() @ wq.double().abs().t() + (0 if b is None else b.double().abs())
+        bound = exact.abs() * ulp + mag * (k + 2) * 2.0 ** -24 + 1e-30
+        err = (y.cpu().double() - exact).abs()
+        assert y.shape == (m, w.shape[0])
+        assert bool((err <= bound).all()), float((err / bound).max())
+
+
+def test_group_launch_one_hot_bit_exact_and_mixed_fallback(gpu):
+    """One-hot rows through the grouped launch give the oracle's qdq(W) bit for bit; a group whose
+    linears differ in kind runs them one after another with the same results."""
+    k = 256
+    g = torch.Generator().manual_seed(5)
+    ws = [(torch.randn(n, k, generator=g) * 0.05).to(torch.bfloat16) for n in (48, 32)]
+    cols = torch.tensor([0, 1, 31, 32, 63, 64, 127, 128, 129, 200, 255, 2, 3, 4, 5, 6])
+    x = torch.zeros(16, k, dtype=torch.bfloat16)
+    x[torch.arange(16), cols] = 1.0
+    for kinds in ((1, 1), (0, 1)):
+        ams = [make_amax(w, "tensor") for w in ws]
+        if kinds[0] != kinds[1]:
+            ys = [ops().qlinear_small_m_group([x.to(gpu)], [w.to(gpu)], [None], [a.to(gpu)], [blk], kd, [8], [0], [0])[0]
+                  for w, (a, blk), kd in zip(ws, ams, kinds)]
+        else:
+            ys = ops().qlinear_small_m_group([x.to(gpu)] * 2, [w.to(gpu) for w in ws], [None, None],
+                                             [a.to(gpu) for a, _ in ams], [blk for _, blk in ams], kinds[0],
+                                             [8, 8], [0, 0], [0, 0])
+        for w, (a, blk), kd, y in zip(ws, ams, kinds, ys):
+            want = oracle_wq(w, a, blk, kd)[:, cols].t().contiguous()
+            assert torch.equal(y.cpu().float(), want.float())
+
+
+@pytest.mark.parametrize("cfg_name", ["FP8_DEFAULT_CFG", "INT4_AWQ_CFG"])
+def test_attention_qkv_projections_run_as_one_launch(gpu, cfg_name, monkeypatch):
+    """A decode step of a quantized HF Llama runs q/k/v_proj as one grouped launch (one take that
+    launches, two that hand out cached outputs) and its logits match the ungrouped fused path."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization.nn.modules import quant_linear as ql
+
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=128, max_position_embeddings=64)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).to(gpu, torch.bfloat16).eval()
+    ids = torch.randint(0, 128, (2, 4, 16), device=gpu)
+    mtq.quantize(model, getattr(mtq, cfg_name), lambda m: [m(b) for b in ids])
+    counts = {"grouped": 0, "cached": 0}
+    real_take = ql.ProjectionGroup.take
+
+    def spy(self, mod, inp):
+        had_key = self.key is not None
+        y = real_take(self, mod, inp)
+        if y is not None:
+            counts["cached" if had_key else "grouped"] += 1
+        return y
+
+    monkeypatch.setattr(ql.ProjectionGroup, "take", spy)
+    x = torch.randint(0, 128, (1, 1), device=gpu)
+    with torch.no_grad():
+        grouped = model(x).logits
+        monkeypatch.setattr(ql.ProjectionGroup, "take", lambda self, mod, inp: None)
+        single = model(x).logits
+    assert counts == {"grouped": 2, "cached": 4}, counts  # per layer: one launch, two cached outputs
+    tol = 2 ** -6
+    assert torch.allclose(grouped.float(), single.float(), rtol=tol, atol=tol * single.float().abs().max().item())

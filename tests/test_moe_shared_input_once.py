@@ -50,3 +50,65 @@ def test_shared_input_once_equals_per_expert(cfg_name, monkeypatch):
     for k in a1:
         assert torch.equal(a1[k], a0[k]), k
     assert torch.equal(l1, l0)
+
+
+class _EPExperts(torch.nn.Module):
+    """A fused-experts module whose router may send a row to the sentinel E (expert parallelism:
+    the expert lives on another rank): such rows reach no local F.linear."""
+
+    def __init__(self, E=3, H=16, inter=24):
+        super().__init__()
+        self.num_experts = E
+        g = torch.Generator().manual_seed(62)
+        self.gate_up_proj = torch.nn.Parameter(torch.randn(E, 2 * inter, H, generator=g) * 0.2)
+        self.down_proj = torch.nn.Parameter(torch.randn(E, H, inter, generator=g) * 0.2)
+
+    def forward(self, hidden_states, top_k_index, top_k_weights):
+        out = torch.zeros_like(hidden_states)
+        for e in range(self.num_experts):
+            tok, pos = torch.where(top_k_index == e)
+            if tok.numel() == 0:
+                continue
+            gate, up = torch.nn.functional.linear(hidden_states[tok], self.gate_up_proj[e]).chunk(2, dim=-1)
+            h = torch.nn.functional.linear(torch.nn.functional.silu(gate) * up, self.down_proj[e])
+            out.index_add_(0, tok, h * top_k_weights[tok, pos, None])
+        return out
+
+
+def _ep_run(force_per_expert, monkeypatch):
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization.plugins import huggingface as hf
+
+    orig = hf._token_separable
+    monkeypatch.setattr(hf, "_token_separable", (lambda q: False) if force_per_expert else orig)
+    g = torch.Generator().manual_seed(63)
+    hs = torch.randn(10, 16, generator=g)
+    hs[3] *= 50.0  # the largest row goes to the sentinel only: it must not set the amax
+    idx = torch.randint(0, 3, (10, 2), generator=g)
+    idx[3] = 3
+    idx[7, 1] = 3  # a row with one local and one remote expert
+    w = torch.rand(10, 2, generator=g)
+
+    class Wrap(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.experts = _EPExperts()
+
+        def forward(self, x):
+            return self.experts(x, idx, w)
+
+    model = mtq.quantize(Wrap(), mtq.FP8_DEFAULT_CFG, lambda m: m(hs))
+    with torch.no_grad():
+        out = model(hs)
+    monkeypatch.setattr(hf, "_token_separable", orig)
+    return model.experts.gate_up_proj_input_quantizer.amax.float(), out, hs[(idx < 3).any(-1)]
+
+
+def test_sentinel_rows_do_not_reach_the_shared_input_amax(monkeypatch):
+    """Rows routed only to the sentinel are excluded from the once-per-forward input amax without
+    a host sync (zeroed on the device): amax and outputs equal the per-expert calls'."""
+    a1, o1, routed = _ep_run(False, monkeypatch)
+    a0, o0, _ = _ep_run(True, monkeypatch)
+    assert torch.equal(a1, routed.abs().amax().float())
+    assert torch.equal(a1, a0)
+    assert torch.isfinite(o1).all() and torch.equal(o1, o0)
