@@ -120,7 +120,7 @@ def run(samples=512, seq=512, batch=16, layers=80, config="MXFP4_DEFAULT_CFG", m
     bf16_s = None
     if baseline:
         # the same forward passes without quantizers (the model's own bf16 cost of calibration)
-        with ctx():
+        with ctx(), torch.no_grad():
             model(batches[0])
         torch.cuda.synchronize()
         if dist.is_initialized():

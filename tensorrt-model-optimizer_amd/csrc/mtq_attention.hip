@@ -103,6 +103,30 @@ __device__ __forceinline__ float e2m1_mag(float a) {
                     : 6.f;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// RN(a / s) for a pair of a >= +0 (or NaN) on the packed fp32 ALU: div_rn (mtq_device.hpp) without
+// its copysign -- p never is -0 -- two quotients per v_pk_mul / v_pk_fma
+__device__ __forceinline__ f2v div_rn_pos2(f2v q, float s, float r) {
+  const f2v sv = {s, s}, rv = {r, r};
+  const f2v y0 = q * rv;
+  const f2v e = __builtin_elementwise_fma(-y0, sv, q);
+  return __builtin_elementwise_fma(e, rv, y0);
+}
+
+// two fp32 -> two packed T (one v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32, RNE); the asm pins the fp32
+// pair so no mixed-precision fma folds the rounding (as Elem<T>::st)
+template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b) {
+  f2v v = {a, b};
+  asm("" : "+v"(v));
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, t2));
+}
+template <typename T> __device__ __forceinline__ f2v unpack2(uint32_t w) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_convertvector(__builtin_bit_cast(t2, w), f2v);
+}
+
 template <typename T, int D, int PQ, int kStage>  // kStage: keys staged in LDS per barrier pair
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
   typedef typename AMma<T>::v8 v8;
@@ -308,17 +332,29 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
       m = mn;
 
       if (PQ == 1) {
-        // ---- FP8 P qdq: e4m3(clamp(p / S, +-448)) * S  (p >= 0)
+        // ---- FP8 P qdq: e4m3(clamp(p / S, +-448)) * S  (p >= +0 or NaN), two keys per packed
+        // divide, per v_cvt_pk_fp8_f32 and per v_cvt_pk_f32_fp8
+        const f2v sp2 = {a.p_scale, a.p_scale};
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          float v = div_rn(p[j], a.p_scale, rs_p);
-          v = v < kE4M3Max ? v : kE4M3Max;
-          p[j] = fp8_rt(v) * a.p_scale;
+        for (int j = 0; j < 16; j += 2) {
+          f2v v = div_rn_pos2(f2v{p[j], p[j + 1]}, a.p_scale, rs_p);
+          v.x = v.x < kE4M3Max ? v.x : kE4M3Max;  // NaN -> 448, as the scalar form
+          v.y = v.y < kE4M3Max ? v.y : kE4M3Max;
+          const int c8 = __builtin_amdgcn_cvt_pk_fp8_f32(v.x, v.y, 0, false);
+          const f2v r = __builtin_amdgcn_cvt_pk_f32_fp8(c8, false) * sp2;
+          p[j] = r.x;
+          p[j + 1] = r.y;
         }
       } else if (PQ == 2) {
         // ---- NVFP4 P qdq: p -> V dtype -> fp32; per 16 keys (j = 8g..8g+7 of both halves)
+        if constexpr (!F32) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) p[j] = Elem<T>::ld(Elem<T>::st(p[j]));
+          for (int j = 0; j < 16; j += 2) {
+            const f2v r = unpack2<T>(pack2<T>(p[j], p[j + 1]));
+            p[j] = r.x;
+            p[j + 1] = r.y;
+          }
+        }
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
           float bmax = 0.f;
@@ -331,11 +367,29 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
           const bool zero = sc == 0.f;
           const float safe = (zero || !(fabsf(sc) < __builtin_inff())) ? 1.f : sc;
           const float rsafe = 1.0f / safe;
+          bool nan = false;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float v = p[8 * g + i];
-            const float qv = e2m1_mag(div_rn(fabsf(v), safe, rsafe)) * safe;
-            p[8 * g + i] = zero ? 0.f : (v >= 0.f ? qv : -qv);
+          for (int i = 0; i < 8; ++i) nan |= p[8 * g + i] != p[8 * g + i];
+          if (!nan) {
+            // p >= +0: |p| / safe rounded to E2M1 by the converter (round half to even on the
+            // E2M1 grid with saturation at 6 = e2m1_mag's thresholds), two keys per convert
+            const f2v sf2 = {safe, safe};
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+              const f2v q = div_rn_pos2(f2v{p[8 * g + i], p[8 * g + i + 1]}, safe, rsafe);
+              const uint32_t c4 = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, q.x, q.y, 1.0f, 0);
+              const auto w = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(c4, 1.0f, 0);
+              const f2v r = f2v{w[0], w[1]} * sf2;
+              p[8 * g + i] = zero ? 0.f : r.x;
+              p[8 * g + i + 1] = zero ? 0.f : r.y;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const float v = p[8 * g + i];
+              const float qv = e2m1_mag(div_rn(fabsf(v), safe, rsafe)) * safe;
+              p[8 * g + i] = zero ? 0.f : (v >= 0.f ? qv : -qv);
+            }
           }
         }
       }
@@ -357,14 +411,23 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
           v8 pb, pb2, pb3;
+          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+          u4v w1, w2, w3;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            pb[i] = Elem<T>::st(p[8 * g + i]);
+          for (int i = 0; i < 8; i += 2) {
+            const float x0 = p[8 * g + i], x1 = p[8 * g + i + 1];
+            w1[i / 2] = pack2<T>(x0, x1);
             if constexpr (SPLIT3) {
-              const float r1 = p[8 * g + i] - Elem<T>::ld(pb[i]);  // exact
-              pb2[i] = Elem<T>::st(r1);
-              pb3[i] = Elem<T>::st(r1 - Elem<T>::ld(pb2[i]));     // exact
+              const f2v r1 = f2v{x0, x1} - unpack2<T>(w1[i / 2]);  // exact
+              w2[i / 2] = pack2<T>(r1.x, r1.y);
+              const f2v r2 = r1 - unpack2<T>(w2[i / 2]);  // exact
+              w3[i / 2] = pack2<T>(r2.x, r2.y);
             }
+          }
+          pb = __builtin_bit_cast(v8, w1);
+          if constexpr (SPLIT3) {
+            pb2 = __builtin_bit_cast(v8, w2);
+            pb3 = __builtin_bit_cast(v8, w3);
           }
 #pragma unroll
           for (int d = 0; d < DB; ++d) {

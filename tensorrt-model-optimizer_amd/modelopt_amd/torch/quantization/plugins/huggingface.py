@@ -98,13 +98,17 @@ class _QuantFusedExperts(QuantModule):
             if d["_down_proj_linear"]:
                 idx = d["_current_expert_idx"]
                 input = self.down_proj_input_quantizer(input)
-                weight = self.down_proj_weight_quantizers[idx](weight)
+                wq = self.down_proj_weight_quantizers[idx]
+                if not _collected_already(wq, weight):
+                    weight = wq(weight)
             else:
                 idx = self._get_expert_idx_from_first_proj(weight)
                 d["_current_expert_idx"] = idx
                 if not d["_first_in_done"]:
                     input = first_in(input)
-                weight = first_w[idx](weight)
+                wq = first_w[idx]
+                if not _collected_already(wq, weight):
+                    weight = wq(weight)
             d["_down_proj_linear"] = not d["_down_proj_linear"]
             return orig_linear(input, weight, bias)
 
@@ -126,6 +130,24 @@ class _QuantFusedExperts(QuantModule):
         for w, q in self.iter_weights_for_calibration():
             if isinstance(q, TensorQuantizer) and q.fake_quant:
                 self._fold_weight_quantizer(q, (w,), keep_attrs)
+
+
+def _collected_already(q, weight) -> bool:
+    """True when calling the weight quantizer ``q`` on ``weight`` would return ``weight`` unchanged
+    and do nothing else: a max calibration pass (collect only, no fake quant, no pre_quant_scale,
+    no block reshape) whose calibrator has just collected this very tensor view at this version
+    (``MaxCalibrator`` skips such a collect; max_calibrate's weight pass collects every expert slice
+    before the forward loop).  Saves the module call per expert and batch of the eager expert loop,
+    whose per-expert host syncs expose every host microsecond."""
+    from ..calib.max import MaxCalibrator
+
+    d = q.__dict__
+    if type(q) is not TensorQuantizer or not d.get("_if_calib") or d.get("_if_quant") or d.get("_disabled"):
+        return False
+    if d.get("_dynamic") or q.pre_quant_scale is not None or q.block_sizes is not None:
+        return False
+    cal = d.get("_calibrator")
+    return type(cal) is MaxCalibrator and cal._acc is not None and cal._same_as_last(weight)
 
 
 def _token_separable(q) -> bool:
