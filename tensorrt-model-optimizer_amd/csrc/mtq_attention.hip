@@ -268,33 +268,43 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
     swrite();
   }
   __syncthreads();
+  constexpr int NSUB = kStage / kKv;
+  // ---- S^T = K . Q^T of one 32-key tile of the staged keys (lane: query fr, keys crow(j, hi))
+  auto score = [&](int sub) -> f32x16 {
+    const unsigned char *const Kt = Ks + sub * kKv * PITCH;
+    f32x16 s;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s[e] = 0.f;
+    if constexpr (F32) {
+#pragma unroll
+      for (int st = 0; st < D / 2; ++st) {
+        const float kv = *reinterpret_cast<const float *>(Kt + fr * PITCH + (2 * st + hi) * 4);
+        s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv, qf32[st], s, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < QS; ++st) {
+        const v8 kf = *reinterpret_cast<const v8 *>(Kt + fr * PITCH + (16 * st + 8 * hi) * 2);
+        s = AMma<T>::mma(kf, qf[st], s);
+      }
+    }
+    return s;
+  };
   for (int t = 0; t < nstages; ++t) {
     if (t + 1 < nstages) gload(t + 1);  // in flight across this stage's math
+    // the scores of tile sub + 1 are issued before the softmax of tile sub (they do not depend on
+    // it): the matrix core works on them while the VALU runs the softmax and the P qdq
+    f32x16 s_next;
+    if (active && t * kStage < w_end) s_next = score(0);
 #pragma unroll
-    for (int sub = 0; sub < kStage / kKv; ++sub) {
+    for (int sub = 0; sub < NSUB; ++sub) {
     const int kv0 = t * kStage + sub * kKv;
-    const unsigned char *const Kt = Ks + sub * kKv * PITCH;
     const unsigned char *const Vt = Vs + sub * kKv * VPITCH;
     // wave-uniform: a tile with no masked (row, key) pair skips the mask arithmetic
     const bool need_mask = kv0 + kKv > lk || (a.causal && kv0 + kKv - 1 > q0 + off);
     if (active && kv0 < w_end) {
-      // ---- S^T = K . Q^T  (lane: query fr, keys crow(j, hi))
-      f32x16 s;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) s[e] = 0.f;
-      if constexpr (F32) {
-#pragma unroll
-        for (int st = 0; st < D / 2; ++st) {
-          const float kv = *reinterpret_cast<const float *>(Kt + fr * PITCH + (2 * st + hi) * 4);
-          s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv, qf32[st], s, 0, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int st = 0; st < QS; ++st) {
-          const v8 kf = *reinterpret_cast<const v8 *>(Kt + fr * PITCH + (16 * st + 8 * hi) * 2);
-          s = AMma<T>::mma(kf, qf[st], s);
-        }
-      }
+      const f32x16 s = s_next;
+      if (sub + 1 < NSUB && kv0 + kKv < w_end) s_next = score(sub + 1);
       float x[16];
       float mloc = kNegInf;
       if (need_mask) {

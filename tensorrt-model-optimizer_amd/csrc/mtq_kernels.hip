@@ -2180,10 +2180,36 @@ __device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restri
   uint32_t b[N];
   constexpr float kInf = __builtin_huge_valf();
   if (__builtin_expect(r0 < kInf && r1 < kInf && s0 < kInf && s1 < kInf, 1)) {
+    // the (row 2p, row 2p+1) pair of column j on the packed ALU: div_rn of both quotients per
+    // v_pk_mul / v_pk_fma (no copysign: a -0 quotient packs as 0 like +0), clamp to [-8, 7] by
+    // v_med3_f32 (clamping before rounding is the same: the bounds are integers), then
+    // RN-to-integer and the two's-complement nibble at once: q + 1.5 * 2^23 has ulp 1, so its low
+    // mantissa bits ARE rint(q) mod 2^22 (one v_pk_add_f32 for the pair).  A NaN quotient (an
+    // infinite weight, an overflowing quotient, a NaN weight) sends the lane to int4_pair_nan.
+    const f32x2_t sv = {s0, s1}, rv = {r0, r1}, magic = {12582912.0f, 12582912.0f};
+    f32x2_t d[N];
+    bool nan = false;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const float x0 = Elem<T>::ld(lo.e[j]), x1 = Elem<T>::ld(hi.e[j]);
-      b[j] = int4_pair_nan(div_rn(x0, s0, r0), x0) | (int4_pair_nan(div_rn(x1, s1, r1), x1) << 4);
+      const f32x2_t q = {Elem<T>::ld(lo.e[j]), Elem<T>::ld(hi.e[j])};
+      const f32x2_t y0 = q * rv;
+      const f32x2_t e = __builtin_elementwise_fma(-y0, sv, q);
+      d[j] = __builtin_elementwise_fma(e, rv, y0);
+      nan |= (d[j].x != d[j].x) | (d[j].y != d[j].y);
+    }
+    if (!nan) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const f32x2_t c = {__builtin_amdgcn_fmed3f(d[j].x, -8.f, 7.f), __builtin_amdgcn_fmed3f(d[j].y, -8.f, 7.f)};
+        const f32x2_t t = c + magic;
+        b[j] = (__float_as_uint(t.x) & 0xFu) | ((__float_as_uint(t.y) << 4) & 0xF0u);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float x0 = Elem<T>::ld(lo.e[j]), x1 = Elem<T>::ld(hi.e[j]);
+        b[j] = int4_pair_nan(d[j].x, x0) | (int4_pair_nan(d[j].y, x1) << 4);
+      }
     }
   } else {
 #pragma unroll

@@ -369,6 +369,17 @@ def force_eager_experts_impl_on_the_fly(model):
     _force(getattr(model, "config", None))
 
 
+_ATTN_MODULES: dict = {}
+
+
+def _attn_module_of(cls):
+    """``inspect.getmodule`` of an attention class, memoised (called on every attention forward)."""
+    mod = _ATTN_MODULES.get(cls)
+    if mod is None:
+        mod = _ATTN_MODULES[cls] = inspect.getmodule(cls)
+    return mod
+
+
 class _QuantAttention(QuantModule):
     """KV-cache / attention-BMM quantization for transformers attention modules that dispatch
     through ``ALL_ATTENTION_FUNCTIONS`` (reference plugins/huggingface.py:78-410).
@@ -465,7 +476,7 @@ class _QuantAttention(QuantModule):
             cfg = next((getattr(m, "config", None) for m in self.children() if hasattr(m, "config")), None)
         impl = getattr(cfg, "_attn_implementation", None) if cfg is not None else None
         eager = impl is None or impl == "eager" or (impl == "sdpa" and kwargs.get("output_attentions", False))
-        module = inspect.getmodule(self.get_attn_type(self))
+        module = _attn_module_of(self.get_attn_type(self))
         eager_fn = getattr(module, "eager_attention_forward", None)
         if eager:
             if eager_fn is None:

@@ -83,6 +83,28 @@ def test_integration_attention_stub_on_device(gpu, p_qdq):
     torch.testing.assert_close(o.cpu()[valid].float(), want[valid].float(), rtol=2e-2, atol=2e-2)
 
 
+def test_integration_qlinear_group_stub_on_device(gpu):
+    """The grouped decode-projection binding of INTEGRATION.md §2d == the torch op's grouped launch
+    (same kernel, same split) bit for bit, for q/k/v-shaped FP8 and INT4-block linears."""
+    from modelopt_amd import _ext
+
+    stub = _integration_stub()
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(3, 512, generator=g).bfloat16().to(gpu)
+    ws = [(torch.randn(n, 512, generator=g) * 0.05).bfloat16().to(gpu) for n in (512, 128, 128)]
+    for kind, nb, blk in ((1, 8, None), (0, 4, 128)):
+        if blk is None:
+            am = [w.float().abs().amax().reshape(()) for w in ws]
+            blocks = [512] * 3
+        else:
+            am = [w.float().reshape(-1, blk).abs().amax(1, keepdim=True) for w in ws]
+            blocks = [blk] * 3
+        ys = stub["qlinear_group"](x, ws, am, blocks, kind, nb)
+        want = _ext.ops().qlinear_small_m_group([x] * 3, ws, [None] * 3, am, blocks, kind, [nb] * 3, [0] * 3, [0] * 3)
+        for y, w in zip(ys, want):
+            assert torch.equal(y, w)
+
+
 def test_integration_stub_reports_errors(gpu):
     stub = _integration_stub()
     x = torch.randn(8, device=gpu, dtype=torch.bfloat16)
