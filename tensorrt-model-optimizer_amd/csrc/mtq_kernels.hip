@@ -2314,7 +2314,18 @@ __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const T *__restr
       amax = (t > amax || t != t) ? t : amax;
     }
   }
-  const float e = mx_e8m0_exponent(amax / 6.0f);
+  // amax / 6 correctly rounded without the IEEE division sequence for 16-bit elements: div_rn
+  // with r = RN(1/6), bit-identical to the operator for every finite bf16 / f16 amax
+  // (scripts/check_div6.c, exhaustive; tests/test_div_rn_check.py); inf / NaN amax keep the
+  // operator's result (inf * RN(1/6) = inf).  fp32 elements keep the division.
+  float d6;
+  if constexpr (N == 8) {
+    constexpr float kInv6 = 1.0f / 6.0f;
+    d6 = amax <= 3.402823466e38f ? div_rn(amax, 6.0f, kInv6) : amax * kInv6;
+  } else {
+    d6 = amax / 6.0f;
+  }
+  const float e = mx_e8m0_exponent(d6);
   if (threadIdx.x % LPB == 0) sc[i / LPB] = (uint8_t)(int)(e + 127.f);
   uint32_t o = 0;
   if constexpr (N == 8) {

@@ -35,3 +35,15 @@ def test_hist_division_matches_ieee_division(tmp_path):
     )
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert "mismatches 0" in r.stdout, r.stdout
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_mxfp4_block_scale_division_matches_ieee(tmp_path):
+    """The MXFP4 export's amax / 6 by div_rn (16-bit elements): every finite 16-bit amax."""
+    exe = tmp_path / "chk_div6"
+    subprocess.run(
+        ["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(REPO / "scripts" / "check_div6.c"), "-lm"],
+        check=True,
+    )
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("mismatches 0"), r.stdout
