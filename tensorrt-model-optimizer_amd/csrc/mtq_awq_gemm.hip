@@ -796,7 +796,9 @@ __global__ __launch_bounds__(256, 1) void awq_search_w4_kernel(AwqGemmArgs p) {
     const int64_t k2 = kof(t + 2);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      // two of tile t+2's sixteen DMA rounds per 8 MFMAs, spread over the phase
+      // two of tile t+2's sixteen DMA rounds per 8 MFMAs, spread over the phase (issuing all sixteen
+      // up front stalls the wave's MFMA issue behind them: 9.9 vs 8.8 ms on gate_proj,
+      // profiles/r03/awq/search_bench_w4_front.json)
       load_a(cur, k2, j);
       load_b(cur, k2, j);
 #pragma unroll
