@@ -131,13 +131,17 @@ template <typename T, int D, int PQ, int kStage>  // kStage: keys staged in LDS 
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
   typedef typename AMma<T>::v8 v8;
   constexpr bool F32 = sizeof(T) == 4;
-  // P . V of NVFP4 is an fp32 ("ieee") dot in the reference.  bf16: P (fp32) is split exactly
-  // into three bf16 terms p = p1 + p2 + p3 (8 significant bits each) and V . p1 + V . p2 + V . p3
-  // runs on the bf16 MFMA -- every product exact, fp32 accumulation, 3 MFMAs of k = 16 instead of
-  // 8 v_mfma_f32_32x32x2_f32.  f16 (whose exponent range cannot hold the small terms) and fp32
-  // q/k/v keep the fp32 MFMA.
-  constexpr bool SPLIT3 = PQ == 2 && !F32 && __is_same(T, __bf16);
-  constexpr bool F32PV = F32 || (PQ == 2 && !SPLIT3);
+  // P . V of NVFP4 is an fp32 ("ieee") dot in the reference.  Its P is c * s_b: an E2M1 value c
+  // (exact in bf16 / f16) times the fp32 scale s_b of the 16-key block b, and a 16-key block is
+  // exactly the k extent of one v_mfma_f32_32x32x16 step, so (FACT) each step multiplies V by the
+  // codes on the 16-bit MFMA (exact products, fp32 sums) into a zero accumulator and adds that
+  // partial times the lane's s_b into O^T with one fma per element (a query's scale is a per-lane
+  // scalar of the O^T layout).  Products c * v are exact either way; the rounding moves from the
+  // reference's RN(c * s_b) per element to one RN per block partial -- fp32-level, far inside the
+  // output dtype's ulp.  (r02 split P into three exact bf16 terms: 3 MFMAs per step.)  fp32 q/k/v
+  // keep the fp32 MFMA.
+  constexpr bool FACT = PQ == 2 && !F32;
+  constexpr bool F32PV = F32;
   constexpr int ES = sizeof(T);
   constexpr int DP = D < 32 ? 32 : D;  // head_dim 16: one 32-wide d block, columns >= D zero
   constexpr int PITCH = DP * ES + 16;  // K row bytes (16-byte pad: conflict-free b128 reads)
@@ -294,8 +298,10 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
     if (t + 1 < nstages) gload(t + 1);  // in flight across this stage's math
     // the scores of tile sub + 1 are issued before the softmax of tile sub (they do not depend on
     // it): the matrix core works on them while the VALU runs the softmax and the P qdq
+    // (not for NVFP4, whose per-block P . V partial needs those 16 registers at D 128, nor fp32)
+    constexpr bool AHEAD = !FACT && !F32;
     f32x16 s_next;
-    if (active && t * kStage < w_end) s_next = score(0);
+    if (AHEAD && active && t * kStage < w_end) s_next = score(0);
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {
     const int kv0 = t * kStage + sub * kKv;
@@ -303,8 +309,8 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
     // wave-uniform: a tile with no masked (row, key) pair skips the mask arithmetic
     const bool need_mask = kv0 + kKv > lk || (a.causal && kv0 + kKv - 1 > q0 + off);
     if (active && kv0 < w_end) {
-      const f32x16 s = s_next;
-      if (sub + 1 < NSUB && kv0 + kKv < w_end) s_next = score(sub + 1);
+      const f32x16 s = AHEAD ? s_next : score(sub);
+      if (AHEAD && sub + 1 < NSUB && kv0 + kKv < w_end) s_next = score(sub + 1);
       float x[16];
       float mloc = kNegInf;
       if (need_mask) {
@@ -341,6 +347,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
         for (int e = 0; e < 16; ++e) acc[d][e] *= corr;
       m = mn;
 
+      float sblk[2] = {1.f, 1.f};  // NVFP4 (FACT): the two 16-key blocks' scales
       if (PQ == 1) {
         // ---- FP8 P qdq: e4m3(clamp(p / S, +-448)) * S  (p >= +0 or NaN), two keys per packed
         // divide, per v_cvt_pk_fp8_f32 and per v_cvt_pk_f32_fp8
@@ -380,10 +387,14 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
           bool nan = false;
 #pragma unroll
           for (int i = 0; i < 8; ++i) nan |= p[8 * g + i] != p[8 * g + i];
+          // FACT: p[] gets the E2M1 values c and sblk[g] the block scale (0 for a zero scale);
+          // otherwise p[] gets c * safe as the reference
+          sblk[g] = zero ? 0.f : safe;
+          const float cs = FACT ? 1.f : safe;
           if (!nan) {
             // p >= +0: |p| / safe rounded to E2M1 by the converter (round half to even on the
             // E2M1 grid with saturation at 6 = e2m1_mag's thresholds), two keys per convert
-            const f2v sf2 = {safe, safe};
+            const f2v sf2 = {cs, cs};
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
               const f2v q = div_rn_pos2(f2v{p[8 * g + i], p[8 * g + i + 1]}, safe, rsafe);
@@ -397,7 +408,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               const float v = p[8 * g + i];
-              const float qv = e2m1_mag(div_rn(fabsf(v), safe, rsafe)) * safe;
+              const float qv = e2m1_mag(div_rn(fabsf(v), safe, rsafe)) * cs;
               p[8 * g + i] = zero ? 0.f : (v >= 0.f ? qv : -qv);
             }
           }
@@ -420,25 +431,11 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
         // is key crow(8g + i, hi)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          v8 pb, pb2, pb3;
           typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-          u4v w1, w2, w3;
+          u4v w1;
 #pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            const float x0 = p[8 * g + i], x1 = p[8 * g + i + 1];
-            w1[i / 2] = pack2<T>(x0, x1);
-            if constexpr (SPLIT3) {
-              const f2v r1 = f2v{x0, x1} - unpack2<T>(w1[i / 2]);  // exact
-              w2[i / 2] = pack2<T>(r1.x, r1.y);
-              const f2v r2 = r1 - unpack2<T>(w2[i / 2]);  // exact
-              w3[i / 2] = pack2<T>(r2.x, r2.y);
-            }
-          }
-          pb = __builtin_bit_cast(v8, w1);
-          if constexpr (SPLIT3) {
-            pb2 = __builtin_bit_cast(v8, w2);
-            pb3 = __builtin_bit_cast(v8, w3);
-          }
+          for (int i = 0; i < 8; i += 2) w1[i / 2] = pack2<T>(p[8 * g + i], p[8 * g + i + 1]);
+          const v8 pb = __builtin_bit_cast(v8, w1);
 #pragma unroll
           for (int d = 0; d < DB; ++d) {
             // elements 0-3: keys 16g + 4hi + 0..3, elements 4-7: keys 16g + 8 + 4hi + 0..3
@@ -449,11 +446,18 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
                 (__attribute__((address_space(3))) v4s *)(base + 8 * VPITCH));
             const v8s w = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
             const v8 vf = __builtin_bit_cast(v8, w);
-            if constexpr (SPLIT3) {  // smallest terms first
-              acc[d] = AMma<T>::mma(vf, pb3, acc[d]);
-              acc[d] = AMma<T>::mma(vf, pb2, acc[d]);
+            if constexpr (FACT) {
+              f32x16 z;
+#pragma unroll
+              for (int e = 0; e < 16; ++e) z[e] = 0.f;
+              const f32x16 part = AMma<T>::mma(vf, pb, z);
+#pragma unroll
+              for (int e = 0; e < 16; ++e) acc[d][e] = __builtin_fmaf(part[e], sblk[g], acc[d][e]);
+              // one 16-register partial live at a time (hoisting the four MFMAs spills at D 128)
+              __builtin_amdgcn_sched_barrier(0);
+            } else {
+              acc[d] = AMma<T>::mma(vf, pb, acc[d]);
             }
-            acc[d] = AMma<T>::mma(vf, pb, acc[d]);
           }
         }
       }
