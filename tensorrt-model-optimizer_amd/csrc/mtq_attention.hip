@@ -127,8 +127,18 @@ template <typename T> __device__ __forceinline__ f2v unpack2(uint32_t w) {
   return __builtin_convertvector(__builtin_bit_cast(t2, w), f2v);
 }
 
+// LDS image sizes of one workgroup (K rows padded, V rows at the tr-read pitch)
+template <typename T, int D, int PQ, int kStage> struct AttnLds {
+  static constexpr bool F32 = sizeof(T) == 4;
+  static constexpr int ES = sizeof(T), DP = D < 32 ? 32 : D;
+  static constexpr int PITCH = DP * ES + 16;
+  static constexpr int VPITCH = F32 ? PITCH : DP * 2 + 4 * ((16 - (DP / 2) % 32 + 32) % 32);
+};
+
+// One 128-row query tile `tile` of (batch b, query head h, KV head kvh).
 template <typename T, int D, int PQ, int kStage>  // kStage: keys staged in LDS per barrier pair
-__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
+__device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int kvh, int tile,
+                                          unsigned char *__restrict__ Ks, unsigned char *__restrict__ Vs) {
   typedef typename AMma<T>::v8 v8;
   constexpr bool F32 = sizeof(T) == 4;
   // P . V of NVFP4 is an fp32 ("ieee") dot in the reference.  Its P is c * s_b: an E2M1 value c
@@ -156,22 +166,9 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
   constexpr int NU = (NCH + kThreads - 1) / kThreads;
   constexpr int DB = DP / 32;  // 32-wide d blocks of O^T
   constexpr int QS = D / 16;  // k steps of S^T
-  __shared__ __attribute__((aligned(16))) unsigned char Ks[kStage * PITCH];
-  __shared__ __attribute__((aligned(16))) unsigned char Vs[kStage * VPITCH];
-
+  static_assert(AttnLds<T, D, PQ, kStage>::VPITCH == VPITCH && AttnLds<T, D, PQ, kStage>::PITCH == PITCH,
+                "LDS layout");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 31, hi = lane >> 5;
-
-  // XCD-contiguous remap (bijective): consecutive ids share an XCD, hence its L2
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int qn = nwg / 8, rr = nwg % 8, xcd = orig % 8;
-  int rem = (xcd < rr ? xcd * (qn + 1) : rr * (qn + 1) + (xcd - rr) * qn) + orig / 8;
-  const int tile = a.tiles_q - 1 - rem % a.tiles_q;  // longest causal tiles first
-  rem /= a.tiles_q;
-  const int hg = rem % a.group;
-  rem /= a.group;
-  const int kvh = rem % a.hkv;
-  const int b = rem / a.hkv;
-  const int h = kvh * a.group + hg;
 
   const int lq = a.len_q[b], lk = a.len_k[b];
   const int r0 = tile * kRowsPerBlock;
@@ -490,6 +487,34 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
   }
 }
 
+// A workgroup runs two query tiles of one (batch, head): the longest and the shortest causal
+// tile of a pair (tiles_q - 1 - p, then p), so every workgroup does the same work and the grid
+// has no long-tile tail (r02 ran one tile per workgroup, longest first: 1:tiles_q work spread).
+template <typename T, int D, int PQ, int kStage>
+__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
+  using L = AttnLds<T, D, PQ, kStage>;
+  __shared__ __attribute__((aligned(16))) unsigned char Ks[kStage * L::PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned char Vs[kStage * L::VPITCH];
+  // XCD-contiguous remap (bijective): consecutive ids share an XCD, hence its L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int qn = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  int rem = (xcd < rr ? xcd * (qn + 1) : rr * (qn + 1) + (xcd - rr) * qn) + orig / 8;
+  const int npair = (a.tiles_q + 1) / 2;
+  const int pr = rem % npair;
+  rem /= npair;
+  const int hg = rem % a.group;
+  rem /= a.group;
+  const int kvh = rem % a.hkv;
+  const int b = rem / a.hkv;
+  const int h = kvh * a.group + hg;
+  const int t_long = a.tiles_q - 1 - pr;
+  attn_tile<T, D, PQ, kStage>(a, b, h, kvh, t_long, Ks, Vs);
+  if (pr < t_long) {  // odd tiles_q: the middle tile runs once
+    __syncthreads();  // the LDS images are re-staged
+    attn_tile<T, D, PQ, kStage>(a, b, h, kvh, pr, Ks, Vs);
+  }
+}
+
 int stage_keys() {  // A/B switch for measurements: MTQ_AMD_ATTN_STAGE=32|64 (default 64)
   static int v = -1;
   if (v < 0) {
@@ -555,7 +580,7 @@ extern "C" int mtq_attention_fwd(const void *q, const void *k, const void *v, vo
     if (strides[i] < 0 || strides[i] % ec) return MTQ_ERR_INVALID_ARG;
   if (max_len_q == 0) return MTQ_OK;
   const int64_t tiles_q = (max_len_q + kRowsPerBlock - 1) / kRowsPerBlock;
-  const int64_t blocks = tiles_q * num_q_heads * (int64_t)batch;
+  const int64_t blocks = (tiles_q + 1) / 2 * num_q_heads * (int64_t)batch;  // two tiles per workgroup
   if (blocks > (int64_t)INT32_MAX) return MTQ_ERR_INVALID_ARG;
   AttnArgs a;
   a.q = q, a.k = k, a.v = v, a.o = o;
