@@ -128,11 +128,16 @@ template <typename T> __device__ __forceinline__ f2v unpack2(uint32_t w) {
 }
 
 // LDS image sizes of one workgroup (K rows padded, V rows at the tr-read pitch)
+// DBUF (16-bit q/k/v): two K/V stages, stage t+1 written while stage t is read -- one barrier per
+// stage instead of two (2 x 37.9 KiB at D 128: two workgroups still fit a CU's 160 KiB)
 template <typename T, int D, int PQ, int kStage> struct AttnLds {
   static constexpr bool F32 = sizeof(T) == 4;
   static constexpr int ES = sizeof(T), DP = D < 32 ? 32 : D;
   static constexpr int PITCH = DP * ES + 16;
   static constexpr int VPITCH = F32 ? PITCH : DP * 2 + 4 * ((16 - (DP / 2) % 32 + 32) % 32);
+  static constexpr bool DBUF = !F32;
+  static constexpr int NBUF = DBUF ? 2 : 1;
+  static constexpr int KIMG = kStage * PITCH, VIMG = kStage * VPITCH;
 };
 
 // One 128-row query tile `tile` of (batch b, query head h, KV head kvh).
@@ -233,14 +238,17 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
       }
     }
   };
-  auto swrite = [&]() {
+  using LD = AttnLds<T, D, PQ, kStage>;
+  auto swrite = [&](int buf) {
+    unsigned char *const kb = Ks + buf * LD::KIMG;
+    unsigned char *const vb = Vs + buf * LD::VIMG;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int c = tid + kThreads * u;
       if (NCH % kThreads == 0 || c < NCH) {
         const int row = c / CR, col = c - row * CR;
-        *reinterpret_cast<uint4 *>(Ks + row * PITCH + col * 16) = kst[u];
-        *reinterpret_cast<uint4 *>(Vs + row * VPITCH + col * 16) = vst[u];
+        *reinterpret_cast<uint4 *>(kb + row * PITCH + col * 16) = kst[u];
+        *reinterpret_cast<uint4 *>(vb + row * VPITCH + col * 16) = vst[u];
       }
     }
   };
@@ -253,9 +261,10 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
   }
 
   if constexpr (DP != D) {  // V columns D..31 are read by the d block and must be zero
-    for (int i = tid; i < kStage * (DP - D); i += kThreads) {
-      const int row = i / (DP - D), col = D + i % (DP - D);
-      *reinterpret_cast<T *>(Vs + row * VPITCH + col * ES) = (T)0.f;
+    for (int i = tid; i < LD::NBUF * kStage * (DP - D); i += kThreads) {
+      const int bi = i / (kStage * (DP - D)), r = i % (kStage * (DP - D));
+      const int row = r / (DP - D), col = D + r % (DP - D);
+      *reinterpret_cast<T *>(Vs + bi * LD::VIMG + row * VPITCH + col * ES) = (T)0.f;
     }
   }
   // ds_read_b64_tr_b16 address of this lane (T10): lane 4q+p of 16-lane group G supplies row
@@ -266,13 +275,14 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
 
   if (nstages > 0) {
     gload(0);
-    swrite();
+    swrite(0);
   }
   __syncthreads();
   constexpr int NSUB = kStage / kKv;
+  const unsigned char *Kb = Ks, *Vb = Vs;  // the stage being read
   // ---- S^T = K . Q^T of one 32-key tile of the staged keys (lane: query fr, keys crow(j, hi))
   auto score = [&](int sub) -> f32x16 {
-    const unsigned char *const Kt = Ks + sub * kKv * PITCH;
+    const unsigned char *const Kt = Kb + sub * kKv * PITCH;
     f32x16 s;
 #pragma unroll
     for (int e = 0; e < 16; ++e) s[e] = 0.f;
@@ -292,6 +302,10 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
     return s;
   };
   for (int t = 0; t < nstages; ++t) {
+    if constexpr (LD::DBUF) {
+      Kb = Ks + (t & 1) * LD::KIMG;
+      Vb = Vs + (t & 1) * LD::VIMG;
+    }
     if (t + 1 < nstages) gload(t + 1);  // in flight across this stage's math
     // the scores of tile sub + 1 are issued before the softmax of tile sub (they do not depend on
     // it): the matrix core works on them while the VALU runs the softmax and the P qdq
@@ -302,7 +316,7 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {
     const int kv0 = t * kStage + sub * kKv;
-    const unsigned char *const Vt = Vs + sub * kKv * VPITCH;
+    const unsigned char *const Vt = Vb + sub * kKv * VPITCH;
     // wave-uniform: a tile with no masked (row, key) pair skips the mask arithmetic
     const bool need_mask = kv0 + kKv > lk || (a.causal && kv0 + kKv - 1 > q0 + off);
     if (active && kv0 < w_end) {
@@ -460,10 +474,17 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
       }
     }
     }
-    __syncthreads();
-    if (t + 1 < nstages) {
-      swrite();
+    if constexpr (LD::DBUF) {
+      // stage t+1 into the other buffer (last read in stage t-1, before the previous barrier),
+      // then one barrier: stage t+1 visible, stage t's reads done before stage t+2 overwrites it
+      if (t + 1 < nstages) swrite((t + 1) & 1);
       __syncthreads();
+    } else {
+      __syncthreads();
+      if (t + 1 < nstages) {
+        swrite(0);
+        __syncthreads();
+      }
     }
   }
 
@@ -493,8 +514,8 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
 template <typename T, int D, int PQ, int kStage>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
   using L = AttnLds<T, D, PQ, kStage>;
-  __shared__ __attribute__((aligned(16))) unsigned char Ks[kStage * L::PITCH];
-  __shared__ __attribute__((aligned(16))) unsigned char Vs[kStage * L::VPITCH];
+  __shared__ __attribute__((aligned(16))) unsigned char Ks[L::NBUF * L::KIMG];
+  __shared__ __attribute__((aligned(16))) unsigned char Vs[L::NBUF * L::VIMG];
   // XCD-contiguous remap (bijective): consecutive ids share an XCD, hence its L2
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int qn = nwg / 8, rr = nwg % 8, xcd = orig % 8;
