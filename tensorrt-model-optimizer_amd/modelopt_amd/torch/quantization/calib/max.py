@@ -43,6 +43,21 @@ def new_collect_epoch() -> None:
     _SHARED = None
 
 
+def quantizer_call_is_noop(q, x) -> bool:
+    """True when calling the TensorQuantizer ``q`` on ``x`` would return ``x`` unchanged and do
+    nothing else: collect-only (max calibration, no fake quant), no pre_quant_scale, no block
+    reshape, and a MaxCalibrator that has just collected this very tensor view at this version (so
+    its collect is skipped).  Lets hot callers (a weight quantizer on every forward of a max
+    calibration pass) skip the module call entirely."""
+    d = q.__dict__
+    if not d.get("_if_calib") or d.get("_if_quant") or d.get("_disabled") or d.get("_dynamic"):
+        return False
+    if d.get("_block_sizes") is not None or q.pre_quant_scale is not None:
+        return False
+    cal = d.get("_calibrator")
+    return type(cal) is MaxCalibrator and cal._acc is not None and cal._same_as_last(x)
+
+
 class MaxCalibrator(_Calibrator):
     """Tracks the absolute max of all collected tensors (per-tensor or along ``axis``)."""
 
@@ -69,22 +84,30 @@ class MaxCalibrator(_Calibrator):
         base = x._base if x._base is not None else x
         return base, (x.storage_offset(), tuple(x.shape), x.stride(), x.dtype)
 
-    def _same_as_last(self, x) -> bool:
+    def _same_as_last(self, x, vk=None) -> bool:
         if self._last is None:
             return False
         ref, key, ver, epoch = self._last
         if epoch != _EPOCH or x.is_inference():
             return False
-        base, k = self._view_key(x)
+        base, k = self._view_key(x) if vk is None else vk
         return ref() is base and k == key and x._version == ver
 
-    @torch.no_grad()
     def collect(self, x):
+        # calibration forwards run under no_grad already: enter the context only when needed
+        # (the decorator form costs several microseconds per call, on every quantizer call)
+        if torch.is_grad_enabled():
+            with torch.no_grad():
+                return self._collect(x)
+        return self._collect(x)
+
+    def _collect(self, x):
         reduce_axis = quant_utils.convert_quantization_axis_to_reduce_axis(x, self._axis)
         if x.device.type == "meta":
             self._meta_amax = quant_utils.amax_view(x, reduce_axis)[4]
             return
-        if self._acc is not None and self._same_as_last(x):
+        vk = None if x.is_inference() else self._view_key(x)
+        if self._acc is not None and vk is not None and self._same_as_last(x, vk):
             return
         keep_shape = quant_utils.amax_view(x, reduce_axis)[4] if reduce_axis is not None else []
         if self._acc is None:
@@ -101,9 +124,9 @@ class MaxCalibrator(_Calibrator):
         self._validated = False
         base = None
         self._last = None
-        if not x.is_inference():  # inference tensors have no version counter
+        if vk is not None:  # inference tensors have no version counter
             try:
-                base, key = self._view_key(x)
+                base, key = vk
                 self._last = (weakref.ref(base), key, x._version, _EPOCH)
             except TypeError:
                 base = None

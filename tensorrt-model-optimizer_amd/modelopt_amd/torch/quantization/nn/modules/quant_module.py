@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from modelopt_amd.torch.utils.distributed import ParallelState
 
+from ...calib.max import quantizer_call_is_noop
 from ...tensor_quant import QUANT_DESC_8BIT_PER_TENSOR
 from .tensor_quantizer import SequentialQuantizer, TensorQuantizer
 
@@ -225,7 +226,10 @@ class QuantLinearConvBase(QuantInputBase):
     def __getattr__(self, name):
         attr = super().__getattr__(name)
         if name == "weight" and self.__dict__.get("_enable_weight_quantization", False):
-            return self._modules["weight_quantizer"](attr)
+            wq = self._modules["weight_quantizer"]
+            if type(wq) is TensorQuantizer and quantizer_call_is_noop(wq, attr):
+                return attr  # max calibration: this weight version is already collected
+            return wq(attr)
         return attr
 
     def forward(self, input, *args, **kwargs):

@@ -309,9 +309,12 @@ class TensorQuantizer(nn.Module):
 
     @property
     def pre_quant_scale(self):
-        if not hasattr(self, "_pre_quant_scale") or not self._enable_pre_quant_scale:
+        # read on every forward: the buffer dict directly (hasattr goes through nn.Module.__getattr__)
+        d = self.__dict__
+        if not d.get("_enable_pre_quant_scale", True):
             return None
-        return self._pre_quant_scale
+        v = d["_buffers"].get("_pre_quant_scale")
+        return v if v is not None else d.get("_pre_quant_scale")
 
     @pre_quant_scale.setter
     def pre_quant_scale(self, value):

@@ -133,21 +133,13 @@ class _QuantFusedExperts(QuantModule):
 
 
 def _collected_already(q, weight) -> bool:
-    """True when calling the weight quantizer ``q`` on ``weight`` would return ``weight`` unchanged
-    and do nothing else: a max calibration pass (collect only, no fake quant, no pre_quant_scale,
-    no block reshape) whose calibrator has just collected this very tensor view at this version
-    (``MaxCalibrator`` skips such a collect; max_calibrate's weight pass collects every expert slice
-    before the forward loop).  Saves the module call per expert and batch of the eager expert loop,
-    whose per-expert host syncs expose every host microsecond."""
-    from ..calib.max import MaxCalibrator
+    """The expert weight quantizer call is a no-op (``calib.max.quantizer_call_is_noop``): a max
+    calibration pass whose calibrator has just collected this very expert slice (max_calibrate's
+    weight pass collects every slice before the forward loop).  Saves the module call per expert
+    and batch of the eager expert loop, whose per-expert host syncs expose every host microsecond."""
+    from ..calib.max import quantizer_call_is_noop
 
-    d = q.__dict__
-    if type(q) is not TensorQuantizer or not d.get("_if_calib") or d.get("_if_quant") or d.get("_disabled"):
-        return False
-    if d.get("_dynamic") or q.pre_quant_scale is not None or q.block_sizes is not None:
-        return False
-    cal = d.get("_calibrator")
-    return type(cal) is MaxCalibrator and cal._acc is not None and cal._same_as_last(weight)
+    return type(q) is TensorQuantizer and quantizer_call_is_noop(q, weight)
 
 
 def _token_separable(q) -> bool:
