@@ -226,19 +226,25 @@ def test_group_launch_one_hot_bit_exact_and_mixed_fallback(gpu):
             assert torch.equal(y.cpu().float(), want.float())
 
 
+@pytest.mark.parametrize("family", ["llama", "qwen2"])  # qwen2: q/k/v projections with biases
 @pytest.mark.parametrize("cfg_name", ["FP8_DEFAULT_CFG", "INT4_AWQ_CFG"])
-def test_attention_qkv_projections_run_as_one_launch(gpu, cfg_name, monkeypatch):
-    """A decode step of a quantized HF Llama runs q/k/v_proj as one grouped launch (one take that
-    launches, two that hand out cached outputs) and its logits match the ungrouped fused path."""
-    from transformers import LlamaConfig, LlamaForCausalLM
+def test_attention_qkv_projections_run_as_one_launch(gpu, cfg_name, family, monkeypatch):
+    """A decode step of a quantized HF Llama / Qwen2 runs q/k/v_proj as one grouped launch (one
+    take that launches, two that hand out cached outputs) and its logits match the ungrouped fused
+    path."""
+    import transformers
 
     import modelopt_amd.torch.quantization as mtq
     from modelopt_amd.torch.quantization.nn.modules import quant_linear as ql
 
-    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
-                      num_key_value_heads=2, vocab_size=128, max_position_embeddings=64)
+    cfg_cls, model_cls = ((transformers.LlamaConfig, transformers.LlamaForCausalLM) if family == "llama"
+                          else (transformers.Qwen2Config, transformers.Qwen2ForCausalLM))
+    cfg = cfg_cls(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                  num_key_value_heads=2, vocab_size=128, max_position_embeddings=64)
     torch.manual_seed(0)
-    model = LlamaForCausalLM(cfg).to(gpu, torch.bfloat16).eval()
+    model = model_cls(cfg).to(gpu, torch.bfloat16).eval()
+    if family == "qwen2":
+        assert model.model.layers[0].self_attn.q_proj.bias is not None
     ids = torch.randint(0, 128, (2, 4, 16), device=gpu)
     mtq.quantize(model, getattr(mtq, cfg_name), lambda m: [m(b) for b in ids])
     counts = {"grouped": 0, "cached": 0}
