@@ -127,6 +127,15 @@ template <typename T> __device__ __forceinline__ f2v unpack2(uint32_t w) {
   return __builtin_convertvector(__builtin_bit_cast(t2, w), f2v);
 }
 
+// buffer descriptor of one K/V stage: wave-uniform base and size (readfirstlane: no waterfall)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stage_rsrc(const void *base, uint32_t bytes) {
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
+
 // LDS image sizes of one workgroup (K rows padded, V rows at the tr-read pitch)
 // DBUF (16-bit q/k/v): two K/V stages, stage t+1 written while stage t is read -- one barrier per
 // stage instead of two (2 x 37.9 KiB at D 128: two workgroups still fit a CU's 160 KiB)
@@ -220,21 +229,42 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
     for (int e = 0; e < 16; ++e) acc[d][e] = 0.f;
   float m = kNegInf, l = 0.f;
 
+  // K/V stage loads by raw buffer loads: the wave-uniform base of stage t (key t * kStage) in the
+  // descriptor, the per-lane row/column offset in ONE loop-invariant VGPR per operand and the
+  // u-th row group in the SGPR soffset.  Keys past the sequence fall outside the descriptor's
+  // num_records (rows_valid * kt * ES bytes; kt >= D is a launch precondition) and read as zero
+  // (0 * garbage could be NaN).  With 64-bit global addresses recomputed per stage, the
+  // allocator reused those address VGPRs as MFMA destinations and every stage waited for its own
+  // prefetch (vmcnt(0)) before the first score MFMA -- the prefetch never overlapped the math.
+  constexpr bool ROWSPLIT = (kThreads % CR) == 0;  // a lane's chunks share its column
+  constexpr int RPU = kThreads / CR;               // rows per u (ROWSPLIT)
+  uint32_t koff[ROWSPLIT ? 1 : NU], voff[ROWSPLIT ? 1 : NU];
+  if constexpr (ROWSPLIT) {
+    koff[0] = (uint32_t)((tid / CR) * a.kt * ES + (tid % CR) * 16);
+    voff[0] = (uint32_t)((tid / CR) * a.vt * ES + (tid % CR) * 16);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int c = tid + kThreads * u, row = c / CR, col = c - (c / CR) * CR;
+      koff[u] = (uint32_t)(row * a.kt * ES + col * 16);
+      voff[u] = (uint32_t)(row * a.vt * ES + col * 16);
+    }
+  }
+  const int kt_b = (int)(a.kt * ES), vt_b = (int)(a.vt * ES);
   uint4 kst[NU], vst[NU];
   auto gload = [&](int t) {
+    int rows = lk - t * kStage;
+    rows = rows < kStage ? rows : kStage;
+    const __amdgpu_buffer_rsrc_t kr = stage_rsrc(K + (int64_t)t * kStage * a.kt, (uint32_t)(rows * kt_b));
+    const __amdgpu_buffer_rsrc_t vr = stage_rsrc(V + (int64_t)t * kStage * a.vt, (uint32_t)(rows * vt_b));
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int c = tid + kThreads * u;
       if (NCH % kThreads == 0 || c < NCH) {
-        const int row = c / CR, col = c - row * CR;
-        const int key = t * kStage + row;
-        if (key < lk) {  // keys past the sequence are zero (0 * garbage could be NaN)
-          kst[u] = *reinterpret_cast<const uint4 *>(K + (int64_t)key * a.kt + col * EC);
-          vst[u] = *reinterpret_cast<const uint4 *>(V + (int64_t)key * a.vt + col * EC);
-        } else {
-          kst[u] = make_uint4(0, 0, 0, 0);
-          vst[u] = make_uint4(0, 0, 0, 0);
-        }
+        const uint32_t ko = ROWSPLIT ? koff[0] : koff[u], vo = ROWSPLIT ? voff[0] : voff[u];
+        const int ks = ROWSPLIT ? u * RPU * kt_b : 0, vs = ROWSPLIT ? u * RPU * vt_b : 0;
+        kst[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(kr, ko, ks, 0));
+        vst[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vr, vo, vs, 0));
       }
     }
   };
@@ -277,6 +307,11 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
     gload(0);
     swrite(0);
   }
+  // vmcnt(0) on EVERY path here: the Q fragment loads above are otherwise waited for only inside
+  // the branch, the compiler's (path-insensitive) wait analysis then keeps them pending at the
+  // loop head, and the first score MFMA of every stage (it reads qf) waited with vmcnt(0) -- for
+  // the stage's own K/V prefetch too, so the prefetch never overlapped the math (ISA-verified)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15
   __syncthreads();
   constexpr int NSUB = kStage / kKv;
   const unsigned char *Kb = Ks, *Vb = Vs;  // the stage being read
@@ -599,6 +634,11 @@ extern "C" int mtq_attention_fwd(const void *q, const void *k, const void *v, vo
   const int64_t ec = dtype == MTQ_F32 ? 4 : 8;  // elements per 16 bytes
   for (int i = 0; i < 12; ++i)  // 16-byte aligned rows: every stride a multiple of 16 bytes
     if (strides[i] < 0 || strides[i] % ec) return MTQ_ERR_INVALID_ARG;
+  // K/V rows are staged by buffer loads bounded per 64-key stage: token rows must not overlap
+  // (token stride >= head_dim) and a stage's span must fit a 31-bit buffer offset
+  const int64_t esz = dtype == MTQ_F32 ? 4 : 2;
+  if (strides[4] < head_dim || strides[7] < head_dim) return MTQ_ERR_INVALID_ARG;
+  if (strides[4] * esz * 64 >= (1ll << 31) || strides[7] * esz * 64 >= (1ll << 31)) return MTQ_ERR_INVALID_ARG;
   if (max_len_q == 0) return MTQ_OK;
   const int64_t tiles_q = (max_len_q + kRowsPerBlock - 1) / kRowsPerBlock;
   const int64_t blocks = (tiles_q + 1) / 2 * num_q_heads * (int64_t)batch;  // two tiles per workgroup
