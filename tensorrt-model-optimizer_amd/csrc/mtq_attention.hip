@@ -136,6 +136,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t stage_rsrc(const void *base, u
   return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
 }
 
+// v op partner(v) for a symmetric op, partner = the lane^32 value: one v_permlane32_swap of v with
+// itself gives each lane its own value in one result and its partner's in the other (lanes 0-31:
+// r[0] own, r[1] partner; lanes 32-63: r[0] partner, r[1] own), so op(r[0], r[1]) needs no select
+// -- replaces __shfl_xor(v, 32) (a ds_bpermute round trip through the LDS and its address math)
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xadd32(float v) {  // own + partner (commutative: same bits)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // LDS image sizes of one workgroup (K rows padded, V rows at the tr-read pitch)
 // DBUF (16-bit q/k/v): two K/V stages, stage t+1 written while stage t is read -- one barrier per
 // stage instead of two (2 x 37.9 KiB at D 128: two workgroups still fit a CU's 160 KiB)
@@ -346,18 +359,9 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
     // it): the matrix core works on them while the VALU runs the softmax and the P qdq
     // (not for NVFP4, whose per-block P . V partial needs those 16 registers at D 128, nor fp32)
     constexpr bool AHEAD = !FACT && !F32;
-    f32x16 s_next;
-    if (AHEAD && active && t * kStage < w_end) s_next = score(0);
-#pragma unroll
-    for (int sub = 0; sub < NSUB; ++sub) {
-    const int kv0 = t * kStage + sub * kKv;
-    const unsigned char *const Vt = Vb + sub * kKv * VPITCH;
-    // wave-uniform: a tile with no masked (row, key) pair skips the mask arithmetic
-    const bool need_mask = kv0 + kKv > lk || (a.causal && kv0 + kKv - 1 > q0 + off);
-    if (active && kv0 < w_end) {
-      const f32x16 s = AHEAD ? s_next : score(sub);
-      if (AHEAD && sub + 1 < NSUB && kv0 + kKv < w_end) s_next = score(sub + 1);
-      float x[16];
+    // ---- pieces of one 32-key softmax tile (the reference's per-BLOCK_N step)
+    // x = s * qk_scale (masked keys -inf); returns the lane's max of x
+    auto scale_x = [&](const f32x16 &s, bool need_mask, int kv0, float (&x)[16]) -> float {
       float mloc = kNegInf;
       if (need_mask) {
 #pragma unroll
@@ -368,32 +372,45 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
           mloc = fmaxf(mloc, x[j]);
         }
       } else {
+        const f2v qs2 = {a.qk_scale, a.qk_scale};  // two scores per v_pk_mul_f32 (same products)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          x[j] = s[j] * a.qk_scale;
-          mloc = fmaxf(mloc, x[j]);
+        for (int j = 0; j < 16; j += 2) {
+          const f2v xv = f2v{s[j], s[j + 1]} * qs2;
+          x[j] = xv.x;
+          x[j + 1] = xv.y;
         }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) mloc = fmaxf(mloc, x[j]);
       }
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
-      const float mn = fmaxf(m, mloc);
-      const float mu = mn == kNegInf ? 0.f : mn;  // rows with no key yet: p = 0, not NaN
-      float p[16];
+      return mloc;
+    };
+    // p = exp2(x - mu) and the lane pair's sum of p (keys in j order, then the partner)
+    auto expsum = [&](const float (&x)[16], float mu, float (&p)[16]) -> float {
       float ls = 0.f;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         p[j] = __builtin_amdgcn_exp2f(x[j] - mu);
         ls += p[j];
       }
-      ls += __shfl_xor(ls, 32);
-      const float corr = m == mn ? 1.f : __builtin_amdgcn_exp2f(m - mu);
-      l = l * corr + ls;
+      return xadd32(ls);
+    };
+    // acc * 1 == acc (NaN included): the rescale runs only when some row of the wave moved its
+    // running max (wave-uniform branch), on packed pairs
+    auto rescale = [&](float corr, bool moved) {
+      if (__builtin_amdgcn_ballot_w64(moved)) {
+        const f2v c2 = {corr, corr};
 #pragma unroll
-      for (int d = 0; d < DB; ++d)
+        for (int d = 0; d < DB; ++d)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[d][e] *= corr;
-      m = mn;
-
-      float sblk[2] = {1.f, 1.f};  // NVFP4 (FACT): the two 16-key blocks' scales
+          for (int e = 0; e < 16; e += 2) {
+            const f2v r = f2v{acc[d][e], acc[d][e + 1]} * c2;
+            acc[d][e] = r.x;
+            acc[d][e + 1] = r.y;
+          }
+      }
+    };
+    // P fake quant in place (sblk: NVFP4's two 16-key block scales for FACT)
+    auto qdq = [&](float (&p)[16], float (&sblk)[2]) {
       if (PQ == 1) {
         // ---- FP8 P qdq: e4m3(clamp(p / S, +-448)) * S  (p >= +0 or NaN), two keys per packed
         // divide, per v_cvt_pk_fp8_f32 and per v_cvt_pk_f32_fp8
@@ -423,7 +440,7 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
           float bmax = 0.f;
 #pragma unroll
           for (int i = 0; i < 8; ++i) bmax = fmaxf(bmax, p[8 * g + i]);
-          bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+          bmax = xmax32(bmax);
           float s8 = div_rn(bmax, six_gs, rs_six);
           s8 = s8 < kE4M3Max ? s8 : kE4M3Max;
           const float sc = fp8_rt(s8) * a.p_scale;
@@ -460,6 +477,9 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
           }
         }
       }
+    };
+    // O^T += V^T . P^T over the 32 keys of Vt
+    auto pv = [&](const float (&p)[16], const float (&sblk)[2], const unsigned char *Vt) {
       if constexpr (F32PV) {
         // ---- O^T += V^T . P^T in fp32 (v_mfma_f32_32x32x2_f32): step tt pairs key crow(tt, 0)
         // (lanes 0-31) with crow(tt, 1) (lanes 32-63)
@@ -490,8 +510,9 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
                 (__attribute__((address_space(3))) v4s *)(base));
             const v4s up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (__attribute__((address_space(3))) v4s *)(base + 8 * VPITCH));
-            const v8s w = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
-            const v8 vf = __builtin_bit_cast(v8, w);
+            typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+            const u2v l2 = __builtin_bit_cast(u2v, lo), u2 = __builtin_bit_cast(u2v, up);
+            const v8 vf = __builtin_bit_cast(v8, u4v{l2.x, l2.y, u2.x, u2.y});
             if constexpr (FACT) {
               f32x16 z;
 #pragma unroll
@@ -507,6 +528,35 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
           }
         }
       }
+    };
+    const int kvs = t * kStage;
+    f32x16 s_a, s_b;  // scores of the stage's two 32-key tiles (fixed registers, no copies)
+    if (AHEAD && active && kvs < w_end) s_a = score(0);
+    {
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+    const int kv0 = kvs + sub * kKv;
+    const unsigned char *const Vt = Vb + sub * kKv * VPITCH;
+    // wave-uniform: a tile with no masked (row, key) pair skips the mask arithmetic
+    const bool need_mask = kv0 + kKv > lk || (a.causal && kv0 + kKv - 1 > q0 + off);
+    if (active && kv0 < w_end) {
+      // tile 1's scores are issued unconditionally (keys past w_end are in LDS: zero or real
+      // data, their scores unused) so no register copy or phi joins the two paths
+      if (AHEAD && NSUB > 1 && sub == 0) s_b = score(1);
+      const f32x16 s = !AHEAD ? score(sub) : (sub == 0 ? s_a : s_b);
+      float x[16], p[16];
+      const float mloc = xmax32(scale_x(s, need_mask, kv0, x));
+      const float mn = fmaxf(m, mloc);
+      const float mu = mn == kNegInf ? 0.f : mn;  // rows with no key yet: p = 0, not NaN
+      const float ls = expsum(x, mu, p);
+      const float corr = m == mn ? 1.f : __builtin_amdgcn_exp2f(m - mu);
+      l = l * corr + ls;
+      rescale(corr, m != mn);
+      m = mn;
+      float sblk[2] = {1.f, 1.f};  // NVFP4 (FACT): the two 16-key blocks' scales
+      qdq(p, sblk);
+      pv(p, sblk, Vt);
+    }
     }
     }
     if constexpr (LD::DBUF) {
