@@ -2375,6 +2375,69 @@ __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const T *__restr
     st_packed_nt(y + i * (N / 2), (uint16_t)o);
 }
 
+// Per-tensor FP8 export (the unified-HF-export weight path): the scale and its reciprocal once per
+// thread from the scalar-loaded amax (the per-vector IEEE 1/s sequence and its wait were ~1.3 VALU
+// per element), the dtype re-rounding as a template parameter instead of a per-element select,
+// and all U vectors of a lane loaded before the first is converted.  Same arithmetic as
+// export_fp8_vec_one: div_rn on packed pairs, optional re-rounding, the native RNE convert for
+// |q| <= 448, the exact per-element form for a lane with an overflowing or NaN quotient.
+template <typename T, bool ROUND>
+__device__ __forceinline__ void export_fp8_pt_one(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y,
+                                                  float s, float r) {
+  constexpr int N = Vec<T>::N;
+  float q[N];
+  bool inrange = true;
+#pragma unroll
+  for (int j = 0; j < N; j += 2) {
+    f32x2_t d = div_rn2((f32x2_t){Elem<T>::ld(v.e[j]), Elem<T>::ld(v.e[j + 1])}, s, r);
+    if constexpr (ROUND) d = round_pair<T>(d);
+    q[j] = d.x;
+    q[j + 1] = d.y;
+    inrange &= (fabsf(d.x) <= kE4M3Max) & (fabsf(d.y) <= kE4M3Max);
+  }
+  if (__builtin_expect(inrange, 1)) {
+    uint32_t w[N / 4];
+#pragma unroll
+    for (int k = 0; k < N / 4; ++k) {
+      int p = __builtin_amdgcn_cvt_pk_fp8_f32(q[4 * k], q[4 * k + 1], 0, false);
+      w[k] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(q[4 * k + 2], q[4 * k + 3], p, true);
+    }
+    if constexpr (N == 8)
+      st_packed_nt(y + i * N, w[0], w[1]);
+    else
+      st_packed_nt(y + i * N, w[0]);
+    return;
+  }
+  uint32_t b[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float qq = div_rn(Elem<T>::ld(v.e[j]), s, r);
+    if constexpr (ROUND) qq = Elem<T>::ld(Elem<T>::st(qq));
+    b[j] = e4m3_byte(qq) | nan_sign_byte(v.e[j]);
+  }
+  if constexpr (N == 8)
+    st_packed_nt(y + i * N, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
+                 b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
+  else
+    st_packed_nt(y + i * N, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
+}
+template <int U, typename T, bool ROUND>
+__global__ __launch_bounds__(kThreads) void export_fp8_pt_kernel(const T *__restrict__ x,
+                                                                  uint8_t *__restrict__ y,
+                                                                  int64_t nvec,
+                                                                  const float *__restrict__ scale) {
+  const float s = scale[0];
+  const float r = 1.0f / s;
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  Vec<T> v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * kThreads < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * Vec<T>::N);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * kThreads < nvec) export_fp8_pt_one<T, ROUND>(base + u * kThreads, v[u], y, s, r);
+}
+
 // U consecutive 256-vector chunks per block (MTQ_AMD_EXPORT_U = 1, 2 or 4; default 2).
 template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__restrict__ x,
@@ -2453,6 +2516,15 @@ int export_native() {
     n = e ? (atoi(e) != 0) : 1;
   }
   return n;
+}
+// MTQ_AMD_EXPORT_FP8_PT=0: per-tensor FP8 export through the generic kernel (A/B)
+int export_fp8_pt() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("MTQ_AMD_EXPORT_FP8_PT");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v;
 }
 unsigned export_grid(int64_t nvec, int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); }
 
@@ -2854,7 +2926,17 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
     if (cols % N == 0 && aligned16(x) && ((uintptr_t)y % N) == 0) {
       const int64_t nvec = n / N, cv = cols / N;
       const FastDiv fcv = make_fastdiv(cv < (1ll << 31) ? (uint32_t)cv : 1u);
-      if (nvec < (1ll << 31))
+      if (!per_row && export_native() && export_fp8_pt())
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          if (round_to_dtype)
+            export_fp8_pt_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+                reinterpret_cast<const T *>(x), y, nvec, scale);
+          else
+            export_fp8_pt_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+                reinterpret_cast<const T *>(x), y, nvec, scale);
+        });
+      else if (nvec < (1ll << 31))
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_fp8_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
