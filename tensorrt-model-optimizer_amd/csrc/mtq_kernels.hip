@@ -1766,6 +1766,60 @@ __global__ __launch_bounds__(kThreads) void nvfp4_native_kernel(const T *__restr
   stg_vec_nt(y + i * N, v);
 }
 
+// U vectors per lane (MTQ_AMD_NVFP4_U, default 2; 1 = nvfp4_native_kernel above): all U loads
+// issued before the first block is converted, and the per-thread constants (global scale, its
+// 6x reciprocal) paid once per U vectors.  Each u-slice is exactly nvfp4_native_kernel's body.
+template <typename T, int BS, int U>
+__global__ __launch_bounds__(kThreads) void nvfp4_native_u_kernel(const T *__restrict__ x,
+                                                                   T *__restrict__ y, int64_t nvec,
+                                                                   const float *__restrict__ gamax) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  static_assert(N == 8 && BS % N == 0, "16-bit elements, block a multiple of the vector");
+  constexpr int LPB = BS / N;
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  const int lead = threadIdx.x % LPB;  // a block's LPB lanes are in range together
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * kThreads - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * N);
+  const float gs = nvfp4_global_scale(gamax);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i - lead >= nvec) continue;
+    uint32_t w[4] = {v[u].raw.x, v[u].raw.y, v[u].raw.z, v[u].raw.w};
+    const PairScan sc = scan_pairs(w);
+    const uint32_t mb = group_max_u32<LPB>(sc.max_abs);
+    const bool block_nan = mb > Fp4Native<T>::kInfBits;
+    float bmax;
+    if (!block_nan) {
+      bmax = half_bits_to_float<T>(mb);
+    } else {
+      float m = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) m = max_skip_nan(m, fabsf(Elem<T>::ld(v[u].e[j])));
+      bmax = group_max_f<LPB>(m);
+    }
+    const Nvfp4Block b = nvfp4_block(bmax, gs);
+    if (!block_nan && !sc.neg_zero) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a0 = div_rn(Elem<T>::ld(v[u].e[2 * j]), b.q, b.r);
+        const float a1 = div_rn(Elem<T>::ld(v[u].e[2 * j + 1]), b.q, b.r);
+        const uint32_t c = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, a0, a1, 1.0f, 0);
+        const auto r = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(c, 1.0f, 0);
+        v[u].e[2 * j] = Elem<T>::st(r[0] * b.q);
+        v[u].e[2 * j + 1] = Elem<T>::st(r[1] * b.q);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j) v[u].e[j] = Elem<T>::st(nvfp4_qdq(Elem<T>::ld(v[u].e[j]), b));
+    }
+    stg_vec_nt(y + i * N, v[u]);
+  }
+}
+
 // any shape: one lane per element of the zero-padded [rows, pcols] matrix, BS lanes per block
 template <typename T, int BS>
 __global__ __launch_bounds__(kThreads) void nvfp4_scalar_kernel(const T *__restrict__ x,
@@ -1798,7 +1852,18 @@ int launch_nvfp4(const T *x, T *y, int64_t rows, int64_t cols, const float *gama
     if constexpr (sizeof(T) == 2) {
       static int nv = -1;  // MTQ_AMD_FP4_EMULATE=1 forces the table emulation (A/B runs)
       if (env_variant("MTQ_AMD_FP4_EMULATE", &nv) == 0) {
-        nvfp4_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec, gamax);
+        static int nu = -1;  // MTQ_AMD_NVFP4_U: vectors per lane (1, 2 or 4; default 2)
+        if (nu < 0) {
+          const char *e = getenv("MTQ_AMD_NVFP4_U");
+          nu = e ? atoi(e) : 2;
+          if (nu != 1 && nu != 2 && nu != 4) nu = 2;
+        }
+        if (nu == 1)
+          nvfp4_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec, gamax);
+        else if (nu == 2)
+          nvfp4_native_u_kernel<T, BS, 2><<<(unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0, stream>>>(x, y, nvec, gamax);
+        else
+          nvfp4_native_u_kernel<T, BS, 4><<<(unsigned)((nvec + 4 * kThreads - 1) / (4 * kThreads)), kThreads, 0, stream>>>(x, y, nvec, gamax);
         return check_launch();
       }
     }
