@@ -73,7 +73,7 @@ struct AttnArgs {
   void *o;
   const int32_t *start_q, *len_q, *start_k, *len_k;
   int64_t qb, qt, qh, kb, kt, kh, vb, vt, vh, ob, ot, oh;  // element strides (batch, token, head)
-  int hkv, group, tiles_q, causal;
+  int hkv, group, tiles_q, causal, ppw;  // ppw: query-tile pairs per workgroup
   float qk_scale, p_scale;
 };
 
@@ -587,15 +587,23 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
           T h[4];
         } pk;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pk.h[i] = Elem<T>::st(div_rn(acc[d][4 * e4 + i], den, rden));
+        for (int i = 0; i < 4; i += 2) {  // div_rn on packed pairs (same ops, same copysign)
+          const f2v sv = {den, den}, rv = {rden, rden};
+          const f2v qv = {acc[d][4 * e4 + i], acc[d][4 * e4 + i + 1]};
+          const f2v y0 = qv * rv;
+          const f2v y = __builtin_elementwise_fma(__builtin_elementwise_fma(-y0, sv, qv), rv, y0);
+          pk.h[i] = Elem<T>::st(__builtin_copysignf(y.x, qv.x));
+          pk.h[i + 1] = Elem<T>::st(__builtin_copysignf(y.y, qv.y));
+        }
         *reinterpret_cast<Pack *>(orow + 32 * d + 8 * e4 + 4 * hi) = pk;
       }
   }
 }
 
-// A workgroup runs two query tiles of one (batch, head): the longest and the shortest causal
-// tile of a pair (tiles_q - 1 - p, then p), so every workgroup does the same work and the grid
-// has no long-tile tail (r02 ran one tile per workgroup, longest first: 1:tiles_q work spread).
+// A workgroup runs ppw pairs of query tiles of one (batch, head), each the longest and the
+// shortest causal tile of a pair (tiles_q - 1 - p, then p), so every workgroup does the same work
+// and the grid has no long-tile tail (r02 ran one tile per workgroup, longest first: 1:tiles_q
+// work spread).  ppw = 1 by default (MTQ_AMD_ATTN_PPW for A/B).
 template <typename T, int D, int PQ, int kStage>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
   using L = AttnLds<T, D, PQ, kStage>;
@@ -606,18 +614,23 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
   const int qn = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   int rem = (xcd < rr ? xcd * (qn + 1) : rr * (qn + 1) + (xcd - rr) * qn) + orig / 8;
   const int npair = (a.tiles_q + 1) / 2;
-  const int pr = rem % npair;
-  rem /= npair;
+  const int ngrp = (npair + a.ppw - 1) / a.ppw;  // pair groups of a (batch, head)
+  const int pg = rem % ngrp;
+  rem /= ngrp;
   const int hg = rem % a.group;
   rem /= a.group;
   const int kvh = rem % a.hkv;
   const int b = rem / a.hkv;
   const int h = kvh * a.group + hg;
-  const int t_long = a.tiles_q - 1 - pr;
-  attn_tile<T, D, PQ, kStage>(a, b, h, kvh, t_long, Ks, Vs);
-  if (pr < t_long) {  // odd tiles_q: the middle tile runs once
-    __syncthreads();  // the LDS images are re-staged
-    attn_tile<T, D, PQ, kStage>(a, b, h, kvh, pr, Ks, Vs);
+  const int p_end = (pg + 1) * a.ppw < npair ? (pg + 1) * a.ppw : npair;
+  for (int pr = pg * a.ppw; pr < p_end; ++pr) {
+    const int t_long = a.tiles_q - 1 - pr;
+    if (pr > pg * a.ppw) __syncthreads();  // the LDS images are re-staged
+    attn_tile<T, D, PQ, kStage>(a, b, h, kvh, t_long, Ks, Vs);
+    if (pr < t_long) {  // odd tiles_q: the middle tile runs once
+      __syncthreads();
+      attn_tile<T, D, PQ, kStage>(a, b, h, kvh, pr, Ks, Vs);
+    }
   }
 }
 
@@ -691,7 +704,16 @@ extern "C" int mtq_attention_fwd(const void *q, const void *k, const void *v, vo
   if (strides[4] * esz * 64 >= (1ll << 31) || strides[7] * esz * 64 >= (1ll << 31)) return MTQ_ERR_INVALID_ARG;
   if (max_len_q == 0) return MTQ_OK;
   const int64_t tiles_q = (max_len_q + kRowsPerBlock - 1) / kRowsPerBlock;
-  const int64_t blocks = (tiles_q + 1) / 2 * num_q_heads * (int64_t)batch;  // two tiles per workgroup
+  // pairs of query tiles per workgroup (MTQ_AMD_ATTN_PPW; default 1 = two tiles per workgroup)
+  static int ppw_env = -1;
+  if (ppw_env < 0) {
+    const char *e = getenv("MTQ_AMD_ATTN_PPW");
+    ppw_env = e ? atoi(e) : 1;
+    if (ppw_env < 1) ppw_env = 1;
+  }
+  const int64_t npair = (tiles_q + 1) / 2;
+  const int ppw = (int)(ppw_env < npair ? ppw_env : npair);
+  const int64_t blocks = (npair + ppw - 1) / ppw * num_q_heads * (int64_t)batch;
   if (blocks > (int64_t)INT32_MAX) return MTQ_ERR_INVALID_ARG;
   AttnArgs a;
   a.q = q, a.k = k, a.v = v, a.o = o;
@@ -704,6 +726,7 @@ extern "C" int mtq_attention_fwd(const void *q, const void *k, const void *v, vo
   a.group = num_q_heads / num_kv_heads;
   a.tiles_q = (int)tiles_q;
   a.causal = is_causal ? 1 : 0;
+  a.ppw = ppw;
   // triton_fa.py:922 `qk_scale = sm_scale * LOG2E` in Python (double), passed as an fp32 scalar
   a.qk_scale = (float)(softmax_scale * 1.44269504088896);
   a.p_scale = (float)p_qdq_scale;
