@@ -545,7 +545,8 @@ __device__ __forceinline__ float mx_qdq(float x, float scale, float unscale, int
 // the block amax is a shuffle-max over LPB adjacent lanes (<= 8 lanes: one DPP row).  FMT >= 0
 // bakes the element format in at compile time (the per-element conversion is the kernel's only
 // real ALU work: with a runtime format it was VALU-bound at ~4.3 TB/s); FMT = -1 reads p.fmt.
-template <typename T, int BS, int FMT>
+// U vectors per lane (MTQ_AMD_MX_U = 1 or 2, default 2): all U loads issued first.
+template <typename T, int BS, int FMT, int U>
 __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ x,
                                                            T *__restrict__ y, int64_t nvec,
                                                            MxParams p) {
@@ -555,25 +556,33 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   static_assert(BS % N == 0, "block must be a multiple of the vector");
   const int fmt = FMT >= 0 ? FMT : p.fmt;
   // nvec % LPB == 0 and kThreads % LPB == 0: the LPB lanes of an MX block are all live or all out
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i - (threadIdx.x % LPB) >= nvec) return;
-  V v = ldg_vec_nt(x + i * N);
-  float m = 0.f;
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  const int lead = threadIdx.x % LPB;
+  V v[U];
 #pragma unroll
-  for (int j = 0; j < N; ++j) m = max_skip_nan(m, clamp_flt_max(fabsf(Elem<T>::ld(v.e[j]))));
-  m = group_max_f<LPB>(m);
-  const int64_t blk = i / LPB;
-  float scale, unscale;
-  if (p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
-    e8m0_scale(m, format_max(fmt), scale, unscale);
-  } else {
-    const int64_t row = (blk * BS) / p.cols;
-    mx_block_scale(m, row, p, scale, unscale);
+  for (int u = 0; u < U; ++u)
+    if (base + u * kThreads - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * N);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i - lead >= nvec) continue;
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) m = max_skip_nan(m, clamp_flt_max(fabsf(Elem<T>::ld(v[u].e[j]))));
+    m = group_max_f<LPB>(m);
+    const int64_t blk = i / LPB;
+    float scale, unscale;
+    if (p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
+      e8m0_scale(m, format_max(fmt), scale, unscale);
+    } else {
+      const int64_t row = (blk * BS) / p.cols;
+      mx_block_scale(m, row, p, scale, unscale);
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      v[u].e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v[u].e[j]), scale, unscale, fmt));
+    stg_vec_nt(y + i * N, v[u]);
   }
-#pragma unroll
-  for (int j = 0; j < N; ++j)
-    v.e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v.e[j]), scale, unscale, fmt));
-  stg_vec_nt(y + i * N, v);
 }
 
 // MXFP4 (E2M1 elements, E8M0 scales, no global amax) on 16-bit inputs with the native CDNA4
@@ -634,14 +643,27 @@ void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t strea
       return;
     }
   }
+  static int mu = -1;  // MTQ_AMD_MX_U: vectors per lane of mx_vec_kernel (1 or 2; default 2)
+  if (mu < 0) {
+    const char *e = getenv("MTQ_AMD_MX_U");
+    mu = (e && atoi(e) == 1) ? 1 : 2;
+  }
+  const unsigned g2 = (unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads));
+  auto go = [&](auto fmt_c) {
+    constexpr int F = decltype(fmt_c)::value;
+    if (mu == 1)
+      mx_vec_kernel<T, BS, F, 1><<<g, kThreads, 0, stream>>>(x, y, nvec, p);
+    else
+      mx_vec_kernel<T, BS, F, 2><<<g2, kThreads, 0, stream>>>(x, y, nvec, p);
+  };
   switch (p.fmt) {
-  case MTQ_E2M1: mx_vec_kernel<T, BS, MTQ_E2M1><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-  case MTQ_E4M3: mx_vec_kernel<T, BS, MTQ_E4M3><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-  case MTQ_E5M2: mx_vec_kernel<T, BS, MTQ_E5M2><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-  case MTQ_INT8: mx_vec_kernel<T, BS, MTQ_INT8><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-  case MTQ_E3M2: mx_vec_kernel<T, BS, MTQ_E3M2><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-  case MTQ_E2M3: mx_vec_kernel<T, BS, MTQ_E2M3><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
-  default: mx_vec_kernel<T, BS, -1><<<g, kThreads, 0, stream>>>(x, y, nvec, p); break;
+  case MTQ_E2M1: go(std::integral_constant<int, MTQ_E2M1>{}); break;
+  case MTQ_E4M3: go(std::integral_constant<int, MTQ_E4M3>{}); break;
+  case MTQ_E5M2: go(std::integral_constant<int, MTQ_E5M2>{}); break;
+  case MTQ_INT8: go(std::integral_constant<int, MTQ_INT8>{}); break;
+  case MTQ_E3M2: go(std::integral_constant<int, MTQ_E3M2>{}); break;
+  case MTQ_E2M3: go(std::integral_constant<int, MTQ_E2M3>{}); break;
+  default: go(std::integral_constant<int, -1>{}); break;
   }
 }
 
@@ -1294,27 +1316,36 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
 // ============================================================================================
 // Dynamic INT-n block quant with optional per-column pre-quant scale (AWQ-lite weight side)
 // ============================================================================================
-template <typename T, int BLK>
+// U vectors per lane (MTQ_AMD_BQD_U = 1 or 2, default 2): all U loads issued first
+template <typename T, int BLK, int U>
 __global__ __launch_bounds__(kThreads) void block_quant_dyn_kernel(
     const T *__restrict__ x, T *__restrict__ y, const T *__restrict__ pqs, int64_t nvec,
     int64_t cols, float max_bound, float min_bound) {
   using V = Vec<T>;
   constexpr int N = V::N;
   constexpr int LPB = BLK / N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i - (threadIdx.x % LPB) >= nvec) return;
-  V v = ldg_vec_nt(x + i * N);
-  if (pqs) {
-    const int64_t col = (i * N) % cols;
-    V s = ldg_vec(pqs + col);
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  const int lead = threadIdx.x % LPB;  // a block's LPB lanes are in range together
+  V v[U];
 #pragma unroll
-    for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(Elem<T>::ld(v.e[j]) * Elem<T>::ld(s.e[j]));
+  for (int u = 0; u < U; ++u)
+    if (base + u * kThreads - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * N);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i - lead >= nvec) continue;
+    if (pqs) {
+      const int64_t col = (i * N) % cols;
+      V s = ldg_vec(pqs + col);
+#pragma unroll
+      for (int j = 0; j < N; ++j) v[u].e[j] = Elem<T>::st(Elem<T>::ld(v[u].e[j]) * Elem<T>::ld(s.e[j]));
+    }
+    uint32_t m = group_max_u32<LPB>(vec_absmax_bits(v[u]));
+    IntQ q = make_intq(__uint_as_float(m), max_bound, min_bound);
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[u].e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v[u].e[j]), q));
+    stg_vec_nt(y + i * N, v[u]);
   }
-  uint32_t m = group_max_u32<LPB>(vec_absmax_bits(v));
-  IntQ q = make_intq(__uint_as_float(m), max_bound, min_bound);
-#pragma unroll
-  for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(int_qdq(Elem<T>::ld(v.e[j]), q));
-  stg_vec_nt(y + i * N, v);
 }
 
 // ============================================================================================
@@ -2777,27 +2808,32 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
         (pqs && !aligned16(pqs)))
       return MTQ_ERR_INVALID_ARG;
     const int64_t nvec = rows * cols / N;
-    unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
     const T *xt = reinterpret_cast<const T *>(x);
     T *yt = reinterpret_cast<T *>(y);
     const T *pt = reinterpret_cast<const T *>(pqs);
+    static int bu = -1;  // MTQ_AMD_BQD_U: vectors per lane (1 or 2; default 2)
+    if (bu < 0) {
+      const char *e = getenv("MTQ_AMD_BQD_U");
+      bu = (e && atoi(e) == 1) ? 1 : 2;
+    }
+    auto go = [&](auto blk_c, auto u_c) {
+      constexpr int BLK = decltype(blk_c)::value, U = decltype(u_c)::value;
+      const unsigned gu = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
+      block_quant_dyn_kernel<T, BLK, U><<<gu, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
+    };
+    auto go_u = [&](auto blk_c) {
+      if (bu == 1)
+        go(blk_c, std::integral_constant<int, 1>{});
+      else
+        go(blk_c, std::integral_constant<int, 2>{});
+    };
     switch (block) {
-    case 32:
-      block_quant_dyn_kernel<T, 32>
-          <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
-      break;
-    case 64:
-      block_quant_dyn_kernel<T, 64>
-          <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
-      break;
-    case 128:
-      block_quant_dyn_kernel<T, 128>
-          <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
-      break;
+    case 32: go_u(std::integral_constant<int, 32>{}); break;
+    case 64: go_u(std::integral_constant<int, 64>{}); break;
+    case 128: go_u(std::integral_constant<int, 128>{}); break;
     case 256:
       if constexpr (N == 8) {
-        block_quant_dyn_kernel<T, 256>
-            <<<g, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
+        go_u(std::integral_constant<int, 256>{});
         break;
       }
       return MTQ_ERR_BLOCKSIZE;
