@@ -362,7 +362,10 @@ int mtq_cpu_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtyp
  * Causal queries are the last b_seq_len[b] positions of the key span.  Rows past b_seq_len[b]
  * are not written.  q/k/v/o bf16, f16 or f32 (dtype), 16-byte aligned, head_dim in {16, 32, 64, 96, 128},
  * num_q_heads % num_kv_heads == 0.  softmax_scale / p_qdq_scale are the Python doubles the
- * reference passes (its fp32 kernel scalars are derived from them the same way). */
+ * reference passes (its fp32 kernel scalars are derived from them the same way).
+ * K/V token strides (strides[4], strides[7]) must be >= head_dim (token rows do not overlap) and
+ * span < 2^31 bytes over 64 tokens: the kernel stages keys by buffer loads bounded per 64-key
+ * stage (MTQ_ERR_INVALID_ARG otherwise; every dense [B, S, H, D] / [B, H, S, D] layout passes). */
 int mtq_attention_fwd(const void *q, const void *k, const void *v, void *o,
                       const int32_t *b_start_loc, const int32_t *b_seq_len,
                       const int32_t *b_start_loc_k, const int32_t *b_seq_len_k, int batch,

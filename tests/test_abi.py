@@ -81,3 +81,32 @@ def test_meta_kernels():
     x = torch.empty(3, 5, device="meta", dtype=torch.bfloat16)
     y = _ext.ops().quantize_op(x, torch.empty((), device="meta"), 8, 4, False, False)
     assert y.shape == x.shape and y.dtype == x.dtype and y.device.type == "meta"
+
+
+def test_attention_stride_preconditions_rejected_without_gpu():
+    """mtq_attention_fwd stages K/V by buffer loads bounded per 64-key stage: token rows must not
+    overlap (token stride >= head_dim) and 64 tokens must span < 2^31 bytes.  Checked before any
+    HIP call (include/mtq_amd.h)."""
+    lib = _ext.kernel_cdll()
+    f = lib.mtq_attention_fwd
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p] * 8 + [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+                                                               ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
+    fake = ctypes.c_void_p(4096)  # 16-byte aligned, never dereferenced
+
+    def call(strides):
+        arr = (ctypes.c_int64 * 12)(*strides)
+        return f(fake, fake, fake, fake, fake, fake, fake, fake, 1, 8, 2, 2, 128,
+                 ctypes.cast(arr, ctypes.c_void_p), 1, 0.088, 0, 0.0, 2, None)
+
+    d = 128
+    dense = [0, 2 * d, d] * 4  # [tokens, heads=2, D]: token stride 2D
+    bad_k = list(dense)
+    bad_k[4] = 64  # K token stride < head_dim: overlapping rows
+    assert call(bad_k) == -1
+    bad_v = list(dense)
+    bad_v[7] = 0
+    assert call(bad_v) == -1
+    huge = list(dense)
+    huge[4] = (1 << 31) // 128  # 64 tokens x 2 B x stride = 2^31 bytes
+    assert call(huge) == -1
