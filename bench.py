@@ -168,7 +168,7 @@ def kernel_suite(ops, xs, steps, warmup):
     return res
 
 
-def attention_suite(iters: int = 20):
+def attention_suite(iters: int = 50):
     """The fused flash attention with softmax-P qdq (mtq_attention_fwd) on a Llama-3-8B
     calibration batch (16 x 512 tokens, 32 / 8 heads, D 128, bf16, causal): MFMA TFLOP/s per P
     mode vs the 2.5 PF dense bf16 peak, beside torch SDPA without P qdq."""
