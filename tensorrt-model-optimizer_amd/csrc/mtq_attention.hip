@@ -246,9 +246,8 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
   // descriptor, the per-lane row/column offset in ONE loop-invariant VGPR per operand and the
   // u-th row group in the SGPR soffset.  Keys past the sequence fall outside the descriptor's
   // num_records (rows_valid * kt * ES bytes; kt >= D is a launch precondition) and read as zero
-  // (0 * garbage could be NaN).  With 64-bit global addresses recomputed per stage, the
-  // allocator reused those address VGPRs as MFMA destinations and every stage waited for its own
-  // prefetch (vmcnt(0)) before the first score MFMA -- the prefetch never overlapped the math.
+  // (0 * garbage could be NaN) without a per-row compare.  Replaces 64-bit global addresses
+  // recomputed per stage (address math and VGPRs: 208 vs 226 at D 128, no spills).
   constexpr bool ROWSPLIT = (kThreads % CR) == 0;  // a lane's chunks share its column
   constexpr int RPU = kThreads / CR;               // rows per u (ROWSPLIT)
   uint32_t koff[ROWSPLIT ? 1 : NU], voff[ROWSPLIT ? 1 : NU];
