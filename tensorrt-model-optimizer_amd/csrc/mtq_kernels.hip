@@ -402,6 +402,40 @@ __global__ __launch_bounds__(kThreads) void ew_group_sk_kernel(const T *__restri
   }
 }
 
+// Long channels of whole vectors (per-row weights: one amax per row of >= 128 vectors): a wave's
+// 64 * U consecutive vectors lie in ONE channel when the channel length is a multiple of 64 * U,
+// so the channel, its amax (one scalar load) and the qdq parameters are wave-uniform -- the
+// per-vector channel division, per-lane amax load and per-vector scale computation of the
+// element-wise kernel disappear.  Lane l of the wave takes vectors wb + l + 64 u (each load
+// instruction covers 1 KiB contiguous).  Requires axis_size * vb == nvec (no outer wrap).
+template <typename T, class Op, int U>
+__global__ __launch_bounds__(kThreads) void ew_rowwave_kernel(const T *__restrict__ x,
+                                                               T *__restrict__ y, int64_t nvec,
+                                                               const float *__restrict__ amax,
+                                                               int64_t vb, Op op) {
+  using V = Vec<T>;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wb = ((int64_t)blockIdx.x * kThreads + (int64_t)w * 64) * U;
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = wb + u * 64 + lane;
+    if (i < nvec) v[u] = ldg_vec_nt(x + i * V::N);
+  }
+  if (wb >= nvec) return;
+  const int64_t c = wb / vb;  // wave-uniform (scalar)
+  const auto q = op.qparam_from(amax[c]);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = wb + u * 64 + lane;
+    if (i < nvec) {
+      Op::apply(v[u], q);
+      stg_vec_nt(y + i * V::N, v[u]);
+    }
+  }
+}
+
 int group_u() {
   static int u = -1;
   if (u < 0) {
@@ -479,6 +513,19 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
         ew_scalar_kernel<T, VecOp<T>><<<gs, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), done, n, op);
       }
+      return check_launch();
+    }
+    // long channels (per-row weights): channel length a multiple of 128 vectors, fp32 amax,
+    // 16-byte aligned, no outer wrap -> wave-uniform channel (MTQ_AMD_GROUP_VARIANT=1 skips)
+    if (gv != 1 && vb >= 128 && vb % 128 == 0 && aligned16(x) && aligned16(y) &&
+        op.amax_dtype == MTQ_F32 && axis_size * vb == n / N && n % N == 0) {
+      constexpr int U = 2;
+      const int64_t nvec = n / N;
+      const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
+      if (nvec > 0)
+        ew_rowwave_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
+            reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
+            reinterpret_cast<const float *>(op.amax), vb, op);
       return check_launch();
     }
     return launch_ew<T>(x, y, n, op, stream);

@@ -121,6 +121,8 @@ def test_int_special_values(gpu):
         ((4, 6, 40), (4, 6, 1)),  # merged leading axes (per-token)
         ((4096, 128), (4096, 1)),  # block-128 view of a weight
         ((33, 24), (33, 1)),  # inner 24 = 3 bf16 vectors
+        ((16, 2048), (16, 1)),  # long rows: wave-uniform channel kernel (ew_rowwave_kernel)
+        ((6, 1024), (6, 1)),  # long rows, 128 bf16 vectors each (the kernel's minimum)
     ],
 )
 def test_int_axis(gpu, dtype, shape, amax_shape):
@@ -205,7 +207,8 @@ def test_e4m3_cast(gpu):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize(
-    "shape,amax_shape", [((64, 256), (64, 1)), ((64, 256), (1, 256)), ((8192, 128), (8192, 1))]
+    "shape,amax_shape",
+    [((64, 256), (64, 1)), ((64, 256), (1, 256)), ((8192, 128), (8192, 1)), ((16, 2048), (16, 1))],
 )
 def test_fp8_axis_and_block(gpu, dtype, shape, amax_shape):
     x = rand_with_edges(shape, dtype, seed=21, scale=2.0)
