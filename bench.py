@@ -19,7 +19,9 @@ Also reported (same JSON line):
   ptq           Llama-3-8B FP8 PTQ wall-clock (512 synthetic samples x 512 tokens; DP over ranks,
                 slowest rank), the bf16 forward of the same batches at N=1, and the difference
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one rank per GPU: under
+torch.distributed.run when RANK is set, otherwise bench.py starts that launcher itself as a child
+process (before touching the GPU) and relays rank 0's JSON line and the exit status.
 """
 
 from __future__ import annotations
@@ -43,22 +45,58 @@ TOKENS, HIDDEN, BLOCK = 32768, 4096, 128
 N_BUF = 4
 
 
-def _dist_init(n_gpus: int):
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n_gpus: int) -> int:
+    """`bench.py --gpus N` run directly (no RANK in the environment): start N ranks through a
+    child `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1), relay rank 0's
+    stdout (the one JSON line) and return the launcher's exit status.  Nothing here touches the
+    GPU, and the parent is not replaced (no exec): the ranks are its children.  Reference
+    pattern: tests/_test_utils/torch/distributed/utils.py:56-67 (spawn_multiprocess_job)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n_gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    print("bench: launching " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=os.environ.copy())
+    lines = [ln for ln in proc.stdout.splitlines() if ln.strip()]
+    for ln in lines:
+        if ln.lstrip().startswith("{"):
+            print(ln, flush=True)
+        else:
+            print(ln, file=sys.stderr, flush=True)
+    if proc.returncode != 0:
+        print(f"bench: a rank failed (launcher exit status {proc.returncode})", file=sys.stderr, flush=True)
+    return proc.returncode
+
+
+def _dist_init(n_gpus: int, device: str):
+    cuda = device == "cuda"
     if n_gpus > 1 or "RANK" in os.environ:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         local = int(os.environ.get("LOCAL_RANK", 0))
-        # MTQ_AMD_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU
-        backend = os.environ.get("MTQ_AMD_DIST_BACKEND", "nccl")
-        dev = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(dev)
+        # MTQ_AMD_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU (or on
+        # the host kernels with --device cpu)
+        backend = os.environ.get("MTQ_AMD_DIST_BACKEND", "nccl" if cuda else "gloo")
+        if cuda:
+            dev = local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
         return dist, dist.get_rank(), dist.get_world_size()
-    torch.cuda.set_device(0)
+    if cuda:
+        torch.cuda.set_device(0)
     return None, 0, 1
 
 
@@ -76,13 +114,13 @@ def _max_over_ranks(dist, v: float) -> float:
     return float(t.item())
 
 
-def make_inputs(seed: int):
-    g = torch.Generator(device="cuda").manual_seed(seed)
+def make_inputs(seed: int, device: str = "cuda", tokens: int = TOKENS):
+    g = torch.Generator(device=device).manual_seed(seed)
     xs = []
     for i in range(N_BUF):
-        x = torch.randn(TOKENS, HIDDEN, device="cuda", dtype=torch.bfloat16, generator=g)
+        x = torch.randn(tokens, HIDDEN, device=device, dtype=torch.bfloat16, generator=g)
         # 0.1 % outlier columns x16
-        cols = torch.randperm(HIDDEN, device="cuda", generator=g)[: HIDDEN // 1000]
+        cols = torch.randperm(HIDDEN, device=device, generator=g)[: HIDDEN // 1000]
         x[:, cols] *= 16
         xs.append(x)
     return xs
@@ -94,10 +132,19 @@ def time_kernel(fn, xs, steps: int, warmup: int, dist=None):
     The mean launch duration comes from one pair of HIP events recorded on the launch stream
     around the whole timed region, divided by `steps` (back-to-back launches, so inter-kernel
     gaps count against it).  Events around every single launch would add their own GPU-side
-    packets to each step (measured: ~4 us per launch on a ~87 us kernel)."""
+    packets to each step (measured: ~4 us per launch on a ~87 us kernel).  Host tensors (the
+    --device cpu rehearsal) are timed by the wall clock alone."""
     outs = [None] * len(xs)
     for i in range(warmup):
         outs[i % len(xs)] = fn(xs[i % len(xs)])
+    if not xs[0].is_cuda:
+        _barrier(dist)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            outs[i % len(xs)] = fn(xs[i % len(xs)])
+        _barrier(dist)
+        wall = time.perf_counter() - t0
+        return wall, wall * 1e3 / steps
     torch.cuda.synchronize()
     _barrier(dist)
     torch.cuda.synchronize()
@@ -338,13 +385,23 @@ def main():
     ap.add_argument("--no-ptq", action="store_true", help="skip the Llama-3-8B FP8 PTQ wall-clock")
     ap.add_argument("--no-c3", action="store_true", help="skip the Llama-3-8B INT4 AWQ-lite PTQ (C3)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
+                    help="cpu = plumbing rehearsal on the product's host kernels (default: cuda when a "
+                    "GPU is visible, else cpu)")
+    ap.add_argument("--tokens", type=int, default=TOKENS, help="rows per rank (default: the K3 workload)")
     args = ap.parse_args()
 
-    dist, rank, world = _dist_init(args.gpus)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
+    device = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    if device == "cpu":  # the GPU-only legs need a device
+        args.no_suite = args.no_ptq = True
+    dist, rank, world = _dist_init(args.gpus, device)
     from modelopt_amd import _ext
 
     ops = _ext.ops()
-    xs = make_inputs(1234 + rank)
+    tokens = args.tokens
+    xs = make_inputs(1234 + rank, device, tokens)
     blk = [x.view(-1, BLOCK).abs().amax(dim=1, keepdim=True).float() for x in xs]
     idx = {id(x): i for i, x in enumerate(xs)}
 
@@ -358,7 +415,7 @@ def main():
     value = total / wall / 1e9
     alg_bytes = n * 4 + (n // BLOCK) * 4  # read x bf16 + write y bf16 + read fp32 amax
     achieved = alg_bytes / (ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic()
+    traffic, traffic_src = load_traffic() if (device == "cuda" and tokens == TOKENS) else (None, None)
 
     out = {
         "metric": "fake-quant G-elem/s (% HBM roofline) + PTQ wall-clock, Llama-3-8B FP8",
@@ -375,11 +432,12 @@ def main():
         "data": "synthetic (seeded randn bf16, 0.1% outlier columns x16; amax precomputed per block)",
         "config": {
             "workload": "FP8 e4m3 static block-128 fake quant-dequant of Llama-3-8B activations "
-            f"[{TOKENS} tokens x {HIDDEN}] bf16 per rank (SURVEY K3)",
-            "tokens_per_rank": TOKENS,
+            f"[{tokens} tokens x {HIDDEN}] bf16 per rank (SURVEY K3)",
+            "tokens_per_rank": tokens,
             "hidden": HIDDEN,
             "block": BLOCK,
-            "parallelism": f"dp{world} (independent shards, no collective)",
+            "parallelism": f"dp{world}",
+            "sharding": "independent row shards per rank, no collective in the timed path",
         },
         "roofline": {
             "bound": "hbm",
@@ -394,6 +452,9 @@ def main():
             "mean_launch_ms": round(ms, 4),
         },
     }
+    if device == "cpu":
+        out["device"] = "cpu (plumbing rehearsal on the product's host kernels: not an MI355X measurement)"
+        out["roofline"]["kernel"] = "mtq_cpu_fake_e4m3fy (host)"
     if rank == 0 and not args.no_suite:
         out["kernels"] = kernel_suite(ops, xs, args.steps, args.warmup)
         out["attention_p_qdq"] = attention_suite()
