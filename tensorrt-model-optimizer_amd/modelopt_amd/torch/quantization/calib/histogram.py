@@ -12,9 +12,12 @@ counts each chunk into a thread-local fp32 histogram -- a count stops at 2^24, w
 back to 2^24 -- and adds the per-thread histograms in thread order in fp32 (measured on torch
 2.10: chunk counts (2^24+, 3, 3) give 16777224, (3, 3, 2^24+) give 16777222).  The kernel counts
 exact integers per chunk; when a call can hold more than 2^24 elements, the chunks are counted
-separately and folded exactly so, with ``torch.get_num_threads()`` threads (the reference's own
-process setting; ``MTQ_AMD_HIST_THREADS`` overrides).  ``MTQ_AMD_HIST_COUNTS=exact`` keeps exact
-integer counts instead.
+separately and folded exactly so, with the calibrator's recorded thread count
+``_histc_threads``: fixed at its first ``collect`` from ``torch.get_num_threads()`` (the
+reference's own process setting; ``MTQ_AMD_HIST_THREADS`` overrides) and saved with the quantizer
+state, so a restored calibrator counts exactly as the one that recorded it whatever the new
+process's ``OMP_NUM_THREADS`` (a torchrun launch sets 1).  ``MTQ_AMD_HIST_COUNTS=exact`` keeps
+exact integer counts instead.
 
 ``compute_amax`` runs on the host like the reference (entropy / MSE / percentile).  The MSE sweep
 reproduces the reference's actual call ``fake_tensor_quant(centers, amax, num_bits, unsigned)``,
@@ -58,6 +61,8 @@ class HistogramCalibrator(_Calibrator):
         self._calib_bin_edges = None
         self._calib_hist = None
         self._torch_hist = torch_hist
+        # chunk count of the >2^24-element histc emulation, recorded at the first collect
+        self._histc_threads = None
         if axis is not None:
             raise NotImplementedError("Calibrator histogram collection only supports per tensor scaling")
         if not torch_hist:
@@ -70,6 +75,8 @@ class HistogramCalibrator(_Calibrator):
     def collect(self, x):
         if x.dtype not in (torch.float32, torch.float16, torch.bfloat16):
             x = x.float()  # the reference histograms x.float() (histogram.py:82); exact for ints
+        if self._histc_threads is None:
+            self._histc_threads = _histc_threads()
         # max|x| (equals the reference's max over the non-zero |x| when skip_zeros, histogram.py:105-112)
         x_max = torch.zeros((), dtype=torch.float32, device=x.device)
         quant_utils.reduce_amax_accumulate(x, x_max, None)
@@ -89,7 +96,7 @@ class HistogramCalibrator(_Calibrator):
             bins = self._num_bins
             hmax = self._calib_bin_edges[-1].to(device=x.device, dtype=torch.float32).reshape(())
             old = self._calib_hist
-        hist = _histc_counts(x, hmax.float().contiguous(), bins, self._skip_zeros)
+        hist = _histc_counts(x, hmax.float().contiguous(), bins, self._skip_zeros, self._histc_threads)
         if old is not None:
             hist[: old.numel()] += old.to(hist.device)
         self._calib_hist = hist
@@ -141,13 +148,15 @@ def _histc_threads() -> int:
     return max(1, int(env)) if env else max(1, torch.get_num_threads())
 
 
-def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bool) -> torch.Tensor:
+def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bool,
+                  threads: int | None = None) -> torch.Tensor:
     """fp32 per-call histogram of |x| over [0, hmax] with torch.histc's CPU accumulation.
 
     Every count of a call with at most 2^24 (kept) elements is exact in fp32 whatever the chunking,
-    so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T`` threads,
-    chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted by its own launch (exact
-    integers), clamped at 2^24 and added into the fp32 result in thread order."""
+    so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T = threads``,
+    default ``_histc_threads()``; chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted
+    by its own launch (exact integers), clamped at 2^24 and added into the fp32 result in thread
+    order."""
     ops = _ops()
     n = x.numel()
     mode = os.environ.get("MTQ_AMD_HIST_COUNTS", "histc")
@@ -166,7 +175,7 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
         counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
         ops.histogram_abs_accumulate(flat, hmax, counts, bins, skip_zeros)
         return counts.float()
-    threads = min(_histc_threads(), -(-kept // _HISTC_GRAIN))
+    threads = min(threads or _histc_threads(), -(-kept // _HISTC_GRAIN))
     chunk = -(-kept // threads)
     starts = [t * chunk for t in range(threads) if t * chunk < kept] + [kept]
     if csum is not None:
@@ -252,6 +261,9 @@ def _reference_call_qdq(centers: torch.Tensor, amax: torch.Tensor, bias: int, nu
     return (out / scale) + bias
 
 
+_warned_mse = [False]
+
+
 def _compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128,
                       device=None):
     """MSE amax (histogram.py:285-325).
@@ -269,6 +281,15 @@ def _compute_amax_mse(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1,
     if calib_bin_edges is None and calib_hist is None:
         return None
     intent = os.environ.get("MTQ_AMD_HIST_MSE", "reference") == "intent"
+    if not intent and not _warned_mse[0]:
+        _warned_mse[0] = True
+        warnings.warn(
+            "HistogramCalibrator 'mse': reproducing the reference's actual candidate quantisation "
+            "(fake_tensor_quant(centers, amax, num_bits, unsigned) binds num_bits to `bias` and "
+            "unsigned to `num_bits`; FP8 raises TypeError) for parity; MTQ_AMD_HIST_MSE=intent "
+            "quantises the candidates with num_bits bits / E4M3 instead.",
+            stacklevel=3,
+        )
     counts = torch.from_numpy(calib_hist[:]).float()
     edges = torch.from_numpy(calib_bin_edges[:]).float()
     if intent and device is not None and device.type == "cuda":

@@ -591,7 +591,9 @@ def _awq_sync_act_scale(awq_modules):
                 continue
             module._if_calib = True
             dtype = h.act_scale.dtype if isinstance(h.act_scale, torch.Tensor) else torch.float32
-            h.act_scale = (a / n_present).to(dtype)
+            # fixed_order_sum_many returns every slice on the first linear's device: back to this
+            # linear's (a model spread over several GPUs by device_map)
+            h.act_scale = (a / n_present).to(device=h.weight_scale.device, dtype=dtype)
             h.dp_group = g
             h._dp_cache_steps = n_present
 

@@ -113,6 +113,16 @@ def _fused_forward(mod, input):
     )
 
 
+def _input_quantizer_pure(mod) -> bool:
+    """The module's input quantizer is a plain function of its input: no calibration collect."""
+    q = mod._modules.get("input_quantizer")
+    if q is None:
+        return True
+    if type(q) is not TensorQuantizer:
+        return False
+    return q._disabled or not q._if_calib
+
+
 class ProjectionGroup:
     """The projections of one attention forward that read the same hidden state (q/k/v_proj):
     the first of them to be called with a short input runs all of them as ONE launch
@@ -136,6 +146,11 @@ class ProjectionGroup:
         if self.tried:
             return None
         self.tried = True  # one attempt per forward
+        # every member's input quantizer is applied to THIS input up front: only when that has no
+        # side effect (a calibrating quantizer would collect a tensor that, for k/v called later
+        # with another input -- cross-attention, a device-moving hook -- is not theirs)
+        if any(not _input_quantizer_pure(m) for m in self.mods):
+            return None
         params = [_fused_params(m, input) for m in self.mods]
         if any(p is None for p in params) or len({p[2][2] for p in params}) != 1:
             return None

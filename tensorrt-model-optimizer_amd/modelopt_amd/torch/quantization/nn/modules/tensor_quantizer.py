@@ -857,6 +857,11 @@ class TensorQuantizer(nn.Module):
 
     def get_modelopt_state(self, properties_only: bool = False) -> dict[str, Any]:
         state = {k: getattr(self, k) for k in self._get_properties_for_modelopt_state()}
+        # the histogram calibrator's recorded histc chunk count (calib/histogram.py): restoring it
+        # reproduces the counts (and the entropy / MSE / percentile amax) in any process
+        threads = getattr(getattr(self, "_calibrator", None), "_histc_threads", None)
+        if threads is not None:
+            state["_histc_threads"] = threads
         if properties_only:
             return state
         state["_pytorch_state_metadata"] = self._get_pytorch_state_metadata()
@@ -865,6 +870,10 @@ class TensorQuantizer(nn.Module):
     def set_from_modelopt_state(self, modelopt_state, properties_only: bool = False):
         for key in modelopt_state.keys() - self._skip_properties_for_save_restore:
             if key == "_pytorch_state_metadata":
+                continue
+            if key == "_histc_threads":
+                if hasattr(self._calibrator, "_histc_threads"):
+                    self._calibrator._histc_threads = modelopt_state[key]
                 continue
             setattr(self, key, modelopt_state[key])
         for key in ["_num_bits", "_axis", "_unsigned"]:

@@ -146,9 +146,10 @@ def _token_separable(q) -> bool:
     """Whether ``q`` treats every row (token) of a [tokens, H] input on its own, so that applying
     it to all tokens at once equals applying it to any cover of the tokens by row subsets: disabled;
     or collecting into a MaxCalibrator per tensor / per last-dim channel; and quantizing with a
-    static per-tensor / per-last-dim amax or dynamic blocks along the last dim only (MX, NVFP4,
-    per-token FP8).  Anything else (dynamic per-tensor amax, static row blocks, histograms,
-    custom backends) keeps the per-expert calls."""
+    static per-tensor / per-last-dim amax or dynamic blocks along the last dim only (MX, NVFP4
+    with a static global amax, per-token FP8).  Anything else (NVFP4 whose global amax is taken
+    from the call's input, dynamic per-tensor amax, static row blocks, histograms, custom
+    backends) keeps the per-expert calls."""
     from ..calib.max import MaxCalibrator
 
     if type(q) is not TensorQuantizer:
@@ -166,6 +167,11 @@ def _token_separable(q) -> bool:
         if bs:
             dims = [k for k in bs if isinstance(k, int)]
             if bs.get("type") != "dynamic" or any(k not in (-1, 1) for k in dims):
+                return False
+            # NVFP4's second-level (per-tensor) scale comes from the global amax: without a static
+            # one it is the amax of whatever tensor the call sees (_get_amax -> reduce_amax), so
+            # all routed tokens at once would differ from each expert's token gather
+            if bs.get("scale_bits") == (4, 3) and getattr(q, "_amax", None) is None:
                 return False
         elif q._dynamic or not last_axis:
             return False

@@ -87,7 +87,8 @@ def fixed_order_sum(t: torch.Tensor, group: DistributedProcessGroup) -> torch.Te
 def fixed_order_sum_many(tensors: list[torch.Tensor], group: DistributedProcessGroup) -> list[torch.Tensor]:
     """``fixed_order_sum`` of many tensors with ONE collective: all are flattened into one fp32
     buffer (every rank must pass the same shapes in the same order), gathered once, summed in
-    rank order and split back (fp32, on the first tensor's device).  AWQ-lite uses it for the
+    rank order and split back (fp32, each slice on its own tensor's device: a model spread over
+    several GPUs keeps every linear's result where the linear lives).  AWQ-lite uses it for the
     act_scale / NaN flags of every linear after the caching pass and for every linear's losses
     after the search pass: two collectives per calibration instead of two or three per linear."""
     if not tensors:
@@ -97,7 +98,7 @@ def fixed_order_sum_many(tensors: list[torch.Tensor], group: DistributedProcessG
     out, off = [], 0
     for t in tensors:
         n = t.numel()
-        out.append(summed[off : off + n].reshape(t.shape))
+        out.append(summed[off : off + n].reshape(t.shape).to(t.device))
         off += n
     return out
 

@@ -266,3 +266,54 @@ def test_attention_qkv_projections_run_as_one_launch(gpu, cfg_name, family, monk
     assert counts == {"grouped": 2, "cached": 4}, counts  # per layer: one launch, two cached outputs
     tol = 2 ** -6
     assert torch.allclose(grouped.float(), single.float(), rtol=tol, atol=tol * single.float().abs().max().item())
+
+
+def _qkv_group(gpu, cfg_name):
+    import modelopt_amd.torch.quantization as mtq
+
+    torch.manual_seed(3)
+    mods = [nn.Linear(256, n).to(gpu, torch.bfloat16) for n in (256, 128, 128)]
+    calib = torch.randn(4, 8, 256, device=gpu, dtype=torch.bfloat16)
+    for m in mods:
+        mtq.quantize(m, getattr(mtq, cfg_name), lambda mm: mm(calib))
+    return mods
+
+
+@pytest.mark.parametrize("cfg_name", ["FP8_DEFAULT_CFG", "INT8_DEFAULT_CFG"])
+def test_projection_group_k_v_with_other_input(gpu, cfg_name):
+    """q launches the group on its input; k/v then called with a DIFFERENT tensor (a
+    cross-attention key_value_states) drop the cached outputs and compute on their own input --
+    outputs equal the ungrouped path, and no input quantizer collected a foreign tensor."""
+    from modelopt_amd.torch.quantization.nn.modules import quant_linear as ql
+
+    mods = _qkv_group(gpu, cfg_name)
+    xq = torch.randn(1, 256, device=gpu, dtype=torch.bfloat16)
+    xkv = torch.randn(1, 256, device=gpu, dtype=torch.bfloat16) * 3
+    with torch.no_grad():
+        want = [mods[0](xq), mods[1](xkv), mods[2](xkv)]
+        grp = ql.ProjectionGroup(mods)
+        for m in mods:
+            m.__dict__["_projection_group"] = grp
+        try:
+            got = [mods[0](xq), mods[1](xkv), mods[2](xkv)]
+        finally:
+            for m in mods:
+                m.__dict__.pop("_projection_group", None)
+    assert grp.key is not None  # q did launch the group
+    for a, b in zip(got, want):
+        tol = 2 ** -6
+        assert torch.allclose(a.float(), b.float(), rtol=tol, atol=tol * b.float().abs().max().item())
+
+
+def test_projection_group_not_used_while_input_quantizers_calibrate(gpu):
+    """A calibrating input quantizer has a side effect (it collects): the group must not apply it to
+    q's input on behalf of k/v -- each collects its own input."""
+    from modelopt_amd.torch.quantization.nn.modules import quant_linear as ql
+
+    mods = _qkv_group(gpu, "FP8_DEFAULT_CFG")
+    for m in mods:
+        m.input_quantizer.enable_calib()
+    assert not any(ql._input_quantizer_pure(m) for m in mods)
+    grp = ql.ProjectionGroup(mods)
+    x = torch.randn(1, 256, device=gpu, dtype=torch.bfloat16)
+    assert grp.take(mods[0], x) is None and grp.key is None

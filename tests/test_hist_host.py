@@ -67,3 +67,24 @@ def test_oracle_mse_matches_reference_run(ref):
         hist = t[f"hist_{c['key']}"].int().numpy()
         edges = t[f"edges_{c['key']}"].numpy()
         assert float(R.compute_amax_mse(hist, edges, 8, False)) == c["mse"], c["key"]
+
+
+def test_histc_thread_count_in_quantizer_state():
+    """The histogram calibrator's recorded chunk count travels with the quantizer state (the GPU
+    test test_gpu_hist_ref.py::test_histc_thread_count_is_recorded_and_restored checks the counts)."""
+    from modelopt_amd.torch.quantization import TensorQuantizer
+    from modelopt_amd.torch.quantization.config import QuantizerAttributeConfig
+
+    q = TensorQuantizer(QuantizerAttributeConfig(num_bits=8, calibrator="histogram"))
+    assert q._calibrator._histc_threads is None
+    assert "_histc_threads" not in q.get_modelopt_state()
+    q._calibrator._histc_threads = 5
+    state = q.get_modelopt_state()
+    assert state["_histc_threads"] == 5
+    r = TensorQuantizer(QuantizerAttributeConfig(num_bits=8, calibrator="histogram"))
+    r.set_from_modelopt_state(state)
+    assert r._calibrator._histc_threads == 5
+    assert "_histc_threads" not in r.__dict__
+    m = TensorQuantizer(QuantizerAttributeConfig(num_bits=8))  # max calibrator: the key is ignored
+    m.set_from_modelopt_state(state)
+    assert not hasattr(m._calibrator, "_histc_threads")

@@ -112,3 +112,18 @@ def test_sentinel_rows_do_not_reach_the_shared_input_amax(monkeypatch):
     assert torch.equal(a1, routed.abs().amax().float())
     assert torch.equal(a1, a0)
     assert torch.isfinite(o1).all() and torch.equal(o1, o0)
+
+
+def test_token_separable_nvfp4_needs_a_static_global_amax():
+    """NVFP4 (dynamic block-16, E4M3 scales): the second-level scale uses the global amax, which
+    without a static `_amax` is taken from the call's own input -- not token-separable then."""
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization.config import QuantizerAttributeConfig
+    from modelopt_amd.torch.quantization.plugins import huggingface as hf
+
+    attrs = next(e["cfg"] for e in mtq.NVFP4_DEFAULT_CFG["quant_cfg"] if e["quantizer_name"] == "*input_quantizer")
+    q = mtq.TensorQuantizer(QuantizerAttributeConfig(**attrs))
+    assert q.block_sizes.get("scale_bits") == (4, 3)
+    assert not hf._token_separable(q)
+    q.amax = torch.tensor(3.0)
+    assert hf._token_separable(q)
