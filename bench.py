@@ -384,6 +384,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-ptq", action="store_true", help="skip the Llama-3-8B FP8 PTQ wall-clock")
     ap.add_argument("--no-c3", action="store_true", help="skip the Llama-3-8B INT4 AWQ-lite PTQ (C3)")
+    ap.add_argument("--c5", action="store_true",
+                    help="also run C5: Mixtral-8x7B FP8 PTQ (93 GB bf16 resident, ~2 min) beside its bf16 forward")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
                     help="cpu = plumbing rehearsal on the product's host kernels (default: cuda when a "
@@ -481,6 +483,19 @@ def main():
             r3["ptq_wall_clock_s"] = round(_max_over_ranks(dist, r3["ptq_wall_clock_s"]), 3)
             r3["calib_tokens_per_s"] = round(512 * 512 / r3["ptq_wall_clock_s"], 1)
             out["ptq_c3"] = r3
+        if args.c5:
+            # C5: Mixtral-8x7B FP8 PTQ over the MoE QuantLinear path (opt-in: builds a 93 GB model)
+            print("bench: C5 Mixtral-8x7B FP8_DEFAULT_CFG PTQ ...", file=sys.stderr, flush=True)
+            torch.cuda.empty_cache()
+            _barrier(dist)
+            with contextlib.redirect_stdout(sys.stderr):
+                r5 = ptq_llama.run(samples=512, seq=512, rank=rank, world=world, baseline=(world == 1),
+                                   model_name="mixtral-8x7b")
+            r5["ptq_wall_clock_s"] = round(_max_over_ranks(dist, r5["ptq_wall_clock_s"]), 3)
+            r5["calib_tokens_per_s"] = round(512 * 512 / r5["ptq_wall_clock_s"], 1)
+            if "bf16_forward_s" in r5:
+                r5["overhead_frac"] = round(r5["ptq_wall_clock_s"] / r5["bf16_forward_s"] - 1.0, 4)
+            out["ptq_c5"] = r5
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_ptq:

@@ -602,7 +602,7 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
 // A workgroup runs ppw pairs of query tiles of one (batch, head), each the longest and the
 // shortest causal tile of a pair (tiles_q - 1 - p, then p), so every workgroup does the same work
 // and the grid has no long-tile tail (r02 ran one tile per workgroup, longest first: 1:tiles_q
-// work spread).  ppw = 1 by default (MTQ_AMD_ATTN_PPW for A/B).
+// work spread).  ppw = 1 (two pairs per workgroup measured no faster, profiles/r03/attention/ppw_ab).
 template <typename T, int D, int PQ, int kStage>
 __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  // >= 2 waves / SIMD
   using L = AttnLds<T, D, PQ, kStage>;
@@ -633,15 +633,6 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(AttnArgs a) {  //
   }
 }
 
-int stage_keys() {  // A/B switch for measurements: MTQ_AMD_ATTN_STAGE=32|64 (default 64)
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("MTQ_AMD_ATTN_STAGE");
-    v = (e && atoi(e) == 32) ? 32 : 64;
-  }
-  return v;
-}
-
 template <typename T, int D, int ST>
 void launch_st(const AttnArgs &a, unsigned grid, int mode, hipStream_t stream) {
   if (mode == 0)
@@ -652,12 +643,11 @@ void launch_st(const AttnArgs &a, unsigned grid, int mode, hipStream_t stream) {
     attn_fwd_kernel<T, D, 2, ST><<<grid, kThreads, 0, stream>>>(a);
 }
 
+// 64 keys per LDS stage (32-key stages at 3 waves / SIMD measured slower: 0.104 vs 0.090 ms,
+// profiles/r03/attention/stage_ab)
 template <typename T, int D>
 int launch_d(const AttnArgs &a, unsigned grid, int mode, hipStream_t stream) {
-  if (stage_keys() == 64)
-    launch_st<T, D, 64>(a, grid, mode, stream);
-  else
-    launch_st<T, D, 32>(a, grid, mode, stream);
+  launch_st<T, D, 64>(a, grid, mode, stream);
   return host_check_launch();
 }
 
@@ -703,15 +693,9 @@ extern "C" int mtq_attention_fwd(const void *q, const void *k, const void *v, vo
   if (strides[4] * esz * 64 >= (1ll << 31) || strides[7] * esz * 64 >= (1ll << 31)) return MTQ_ERR_INVALID_ARG;
   if (max_len_q == 0) return MTQ_OK;
   const int64_t tiles_q = (max_len_q + kRowsPerBlock - 1) / kRowsPerBlock;
-  // pairs of query tiles per workgroup (MTQ_AMD_ATTN_PPW; default 1 = two tiles per workgroup)
-  static int ppw_env = -1;
-  if (ppw_env < 0) {
-    const char *e = getenv("MTQ_AMD_ATTN_PPW");
-    ppw_env = e ? atoi(e) : 1;
-    if (ppw_env < 1) ppw_env = 1;
-  }
+  // one pair of query tiles (the longest and the shortest causal tile) per workgroup
   const int64_t npair = (tiles_q + 1) / 2;
-  const int ppw = (int)(ppw_env < npair ? ppw_env : npair);
+  const int ppw = 1;
   const int64_t blocks = (npair + ppw - 1) / ppw * num_q_heads * (int64_t)batch;
   if (blocks > (int64_t)INT32_MAX) return MTQ_ERR_INVALID_ARG;
   AttnArgs a;

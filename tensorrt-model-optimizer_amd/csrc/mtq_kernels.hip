@@ -39,7 +39,6 @@ int num_cus() {
   return cached[dev];
 }
 
-int env_variant(const char *name, int *cache);
 
 unsigned grid_for(int64_t work_items, int per_block) {
   int64_t blocks = (work_items + per_block - 1) / per_block;
@@ -79,7 +78,9 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // Launch structure (measured with scripts/bw_probe.hip on MI355X, bf16 256 MiB in + out):
 // one 16-byte vector per lane, each block a contiguous chunk of 256*U vectors, one chunk per
 // block (no grid-stride loop), reaches 6.1 TB/s; a grid-stride loop with 4 vectors in flight per
-// lane over 2048 blocks only 4.3-4.6 TB/s.  `variant` selects U / non-temporal for tuning.
+// lane over 2048 blocks only 4.3-4.6 TB/s.  U = 1 with non-temporal loads / stores is the one
+// shipped: best of the r01 sweep (scripts/sweep_ew.py: fp8 per-tensor 6.28 TB/s, fp8 block-128
+// 6.0 TB/s vs 5.9 / 5.87 with temporal accesses; U = 2 / 4 no faster).
 template <typename T, class Op, int U, bool NT>
 __global__ __launch_bounds__(kThreads) void ew_vec_kernel(const T *__restrict__ x,
                                                            T *__restrict__ y, int64_t nvec,
@@ -106,15 +107,6 @@ __global__ __launch_bounds__(kThreads) void ew_vec_kernel(const T *__restrict__ 
   }
 }
 
-int ew_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("MTQ_AMD_EW_VARIANT");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 template <typename T, class Op>
 __global__ __launch_bounds__(kThreads) void ew_scalar_kernel(const T *__restrict__ x,
                                                               T *__restrict__ y, int64_t begin,
@@ -133,16 +125,8 @@ int launch_ew(const void *xv, void *yv, int64_t n, Op op, hipStream_t stream) {
   constexpr int N = Vec<T>::N;
   int64_t nvec = (aligned16(x) && aligned16(y)) ? n / N : 0;
   if (nvec > 0) {
-    auto blocks = [&](int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); };
-    // variant 0 (default): U = 1, non-temporal -- best of the r01 sweep (scripts/sweep_ew.py:
-    // fp8 per-tensor 6.28 TB/s, fp8 block-128 6.0 TB/s vs 5.9 / 5.87 for U = 1 temporal)
-    switch (ew_variant()) {
-    case 1: ew_vec_kernel<T, Op, 2, false><<<blocks(2), kThreads, 0, stream>>>(x, y, nvec, op); break;
-    case 2: ew_vec_kernel<T, Op, 1, false><<<blocks(1), kThreads, 0, stream>>>(x, y, nvec, op); break;
-    case 3: ew_vec_kernel<T, Op, 2, true><<<blocks(2), kThreads, 0, stream>>>(x, y, nvec, op); break;
-    case 4: ew_vec_kernel<T, Op, 4, true><<<blocks(4), kThreads, 0, stream>>>(x, y, nvec, op); break;
-    default: ew_vec_kernel<T, Op, 1, true><<<blocks(1), kThreads, 0, stream>>>(x, y, nvec, op); break;
-    }
+    const unsigned blocks = (unsigned)((nvec + kThreads - 1) / kThreads);
+    ew_vec_kernel<T, Op, 1, true><<<blocks, kThreads, 0, stream>>>(x, y, nvec, op);
   }
   int64_t done = nvec * N;
   if (done < n) {
@@ -360,8 +344,8 @@ __global__ __launch_bounds__(kThreads) void ew_group_kernel(const T *__restrict_
   }
 }
 
-// Default for fp32 amax with channel = vector / VB (no wrap; MTQ_AMD_GROUP_VARIANT=3 selects the
-// per-lane-load kernel above for A/B): the wave's 64 / LPB channel amax values arrive through
+// Default for fp32 amax with channel = vector / VB (no wrap; the per-lane-load kernel above
+// otherwise): the wave's 64 / LPB channel amax values arrive through
 // scalar loads from one wave-uniform address (scalar cache, no vector-memory instruction, no
 // per-lane address) and each lane selects its own.  FP8 block-128 bf16 [32768, 4096]: 88.3 ->
 // 83.4-84.9 us (76.6 -> 79.7-81.1 % of HBM peak, profiles/r02/export/).
@@ -436,24 +420,6 @@ __global__ __launch_bounds__(kThreads) void ew_rowwave_kernel(const T *__restric
   }
 }
 
-int group_u() {
-  static int u = -1;
-  if (u < 0) {
-    const char *e = getenv("MTQ_AMD_GROUP_U");
-    u = e ? atoi(e) : 2;
-  }
-  return u;
-}
-
-int group_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("MTQ_AMD_GROUP_VARIANT");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 // --------------------------------------------------------------------------------------------
 // Axis dispatch shared by INT and FP8
 // --------------------------------------------------------------------------------------------
@@ -476,34 +442,26 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
     // channel spans 16..64 vectors (LPB = 8..32 lanes) and the buffers are 16-byte aligned;
     // the vector tail n % N goes through the scalar kernel as in launch_ew.
     const int64_t vb = op.inner_vec64;
-    const int gv = group_variant();
-    if (gv != 1 && vb >= 16 && vb <= 64 && (vb & (vb - 1)) == 0 && aligned16(x) && aligned16(y)) {
+    if (vb >= 16 && vb <= 64 && (vb & (vb - 1)) == 0 && aligned16(x) && aligned16(y)) {
+      // U = 2 vectors per lane (LPB = VB / 2 lanes per channel); U = 1 / 4 measured slower
+      // (74 / 56 % vs ~80 %, profiles/r02/round_c/group_u_ab.json)
       constexpr int U = 2;
       const int64_t nvec = n / N;
       const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
-      const bool sk = gv != 3 && op.amax_dtype == MTQ_F32 && op.small && axis_size * vb == nvec;
+      const bool sk = op.amax_dtype == MTQ_F32 && op.small && axis_size * vb == nvec;
       if (nvec > 0 && sk) {
-        // vectors per lane: U = 2 by default; MTQ_AMD_GROUP_U = 1 or 4 for A/B (LPB = VB / U)
-        auto go = [&](auto uc, auto lc) {
-          constexpr int UU = decltype(uc)::value, L = decltype(lc)::value;
-          const unsigned gg = (unsigned)((nvec + (int64_t)kThreads * UU - 1) / ((int64_t)kThreads * UU));
-          ew_group_sk_kernel<T, VecOp<T>, UU, L><<<gg, kThreads, 0, stream>>>(
+        auto go = [&](auto lc) {
+          constexpr int L = decltype(lc)::value;
+          ew_group_sk_kernel<T, VecOp<T>, U, L><<<g, kThreads, 0, stream>>>(
               reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
               reinterpret_cast<const float *>(op.amax), axis_size, op);
         };
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        using I4 = std::integral_constant<int, 4>;
-        const int gu = group_u();
-        if (vb == 16) {
-          if (gu == 1) go(I1{}, std::integral_constant<int, 16>{});
-          else if (gu == 4) go(I4{}, std::integral_constant<int, 4>{});
-          else go(I2{}, std::integral_constant<int, 8>{});
-        } else if (vb == 32) {
-          go(I2{}, std::integral_constant<int, 16>{});
-        } else {
-          go(I2{}, std::integral_constant<int, 32>{});
-        }
+        if (vb == 16)
+          go(std::integral_constant<int, 8>{});
+        else if (vb == 32)
+          go(std::integral_constant<int, 16>{});
+        else
+          go(std::integral_constant<int, 32>{});
       } else if (nvec > 0)
         ew_group_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec, (int)(vb / U), op);
@@ -516,8 +474,8 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
       return check_launch();
     }
     // long channels (per-row weights): channel length a multiple of 128 vectors, fp32 amax,
-    // 16-byte aligned, no outer wrap -> wave-uniform channel (MTQ_AMD_GROUP_VARIANT=1 skips)
-    if (gv != 1 && vb >= 128 && vb % 128 == 0 && aligned16(x) && aligned16(y) &&
+    // 16-byte aligned, no outer wrap -> wave-uniform channel
+    if (vb >= 128 && vb % 128 == 0 && aligned16(x) && aligned16(y) &&
         op.amax_dtype == MTQ_F32 && axis_size * vb == n / N && n % N == 0) {
       constexpr int U = 2;
       const int64_t nvec = n / N;
@@ -592,7 +550,8 @@ __device__ __forceinline__ float mx_qdq(float x, float scale, float unscale, int
 // the block amax is a shuffle-max over LPB adjacent lanes (<= 8 lanes: one DPP row).  FMT >= 0
 // bakes the element format in at compile time (the per-element conversion is the kernel's only
 // real ALU work: with a runtime format it was VALU-bound at ~4.3 TB/s); FMT = -1 reads p.fmt.
-// U vectors per lane (MTQ_AMD_MX_U = 1 or 2, default 2): all U loads issued first.
+// U = 2 vectors per lane, both loads issued first (MXFP8 0.727 -> 0.754-0.766 of the HBM
+// roofline over one vector per lane, profiles/r03/dyn_u/).
 template <typename T, int BS, int FMT, int U>
 __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ x,
                                                            T *__restrict__ y, int64_t nvec,
@@ -683,25 +642,15 @@ template <typename T, int BS>
 void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t stream) {
   const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
   if constexpr (sizeof(T) == 2) {
-    static int nv = -1;  // MTQ_AMD_FP4_EMULATE=1 forces the table emulation (A/B runs)
-    if (p.fmt == MTQ_E2M1 && p.gamax == nullptr && p.sfmt == MTQ_E8M0 &&
-        env_variant("MTQ_AMD_FP4_EMULATE", &nv) == 0) {
+    if (p.fmt == MTQ_E2M1 && p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
       mx_e2m1_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec);
       return;
     }
   }
-  static int mu = -1;  // MTQ_AMD_MX_U: vectors per lane of mx_vec_kernel (1 or 2; default 2)
-  if (mu < 0) {
-    const char *e = getenv("MTQ_AMD_MX_U");
-    mu = (e && atoi(e) == 1) ? 1 : 2;
-  }
   const unsigned g2 = (unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads));
   auto go = [&](auto fmt_c) {
     constexpr int F = decltype(fmt_c)::value;
-    if (mu == 1)
-      mx_vec_kernel<T, BS, F, 1><<<g, kThreads, 0, stream>>>(x, y, nvec, p);
-    else
-      mx_vec_kernel<T, BS, F, 2><<<g2, kThreads, 0, stream>>>(x, y, nvec, p);
+    mx_vec_kernel<T, BS, F, 2><<<g2, kThreads, 0, stream>>>(x, y, nvec, p);
   };
   switch (p.fmt) {
   case MTQ_E2M1: go(std::integral_constant<int, MTQ_E2M1>{}); break;
@@ -781,7 +730,7 @@ __device__ __forceinline__ uint32_t vec_absmax_bits(const Vec<T> &v) {
   return m;
 }
 
-// Per-tensor (K = 1, Q = 1), grid-stride form (variant 1): wave max, block max in LDS, one
+// Per-tensor (K = 1, Q = 1), grid-stride form (unaligned inputs): wave max, block max in LDS, one
 // atomicMax per block on the fp32 bit pattern.
 __device__ __forceinline__ void block_atomic_max(uint32_t m, uint32_t *out) {
   __shared__ uint32_t red[kThreads / 64];
@@ -867,15 +816,6 @@ __global__ __launch_bounds__(kAmaxThreads) void amax_persist_kernel(const T *__r
   }
 }
 
-int amax_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("MTQ_AMD_AMAX_VARIANT");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 template <typename T, int U>
 int launch_amax_persist(const T *x, int64_t n, int64_t nvec, uint32_t *out, int per_cu,
                         hipStream_t stream) {
@@ -885,68 +825,6 @@ int launch_amax_persist(const T *x, int64_t n, int64_t nvec, uint32_t *out, int 
   if (blocks < 1) blocks = 1;
   amax_persist_kernel<T, U><<<(unsigned)blocks, kAmaxThreads, 0, stream>>>(x, n, nvec, out);
   return check_launch();
-}
-
-// Rows: x viewed as [R, Q] contiguous rows (R = P*K), out[r % K].  G lanes per row (G = 64
-// for long rows, fewer for short ones), each row optionally split into `chunks` pieces handled
-// by different groups; one atomicMax per (row, chunk).
-template <typename T, int G>
-__global__ __launch_bounds__(kThreads) void amax_rows_kernel(const T *__restrict__ x, int64_t R,
-                                                              int64_t Q, int64_t K,
-                                                              int64_t chunk_vec, int64_t chunks,
-                                                              uint32_t *out) {
-  using V = Vec<T>;
-  constexpr int N = V::N;
-  const int64_t qvec = Q / N;
-  const int64_t items = R * chunks;
-  const int64_t groups_total = (int64_t)gridDim.x * (kThreads / G);
-  const int gl = threadIdx.x % G;
-  for (int64_t it = (int64_t)blockIdx.x * (kThreads / G) + threadIdx.x / G; it < items;
-       it += groups_total) {
-    const int64_t r = it / chunks, c = it - r * chunks;
-    const int64_t v0 = c * chunk_vec;
-    int64_t v1 = v0 + chunk_vec;
-    v1 = v1 < qvec ? v1 : qvec;
-    const T *row = x + r * Q;
-    uint32_t m = 0;
-    for (int64_t v = v0 + gl; v < v1; v += G) {
-      uint32_t b = vec_absmax_bits(ldg_vec(row + v * N));
-      m = b > m ? b : m;
-    }
-    m = group_max_u32<G>(m);
-    if (gl == 0) atomicMax(out + (r % K), m);
-  }
-}
-
-// Columns: x viewed as [P, K] (Q = 1, K % N == 0), out[k] over p.  Each lane owns one vector
-// of N consecutive columns and a slab of rows.
-template <typename T>
-__global__ __launch_bounds__(kThreads) void amax_cols_kernel(const T *__restrict__ x, int64_t P,
-                                                              int64_t K, int64_t rows_per_slab,
-                                                              uint32_t *out) {
-  using V = Vec<T>;
-  constexpr int N = V::N;
-  const int64_t kvec = K / N;
-  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t slabs = (P + rows_per_slab - 1) / rows_per_slab;
-  if (t >= kvec * slabs) return;
-  const int64_t s = t / kvec, kv = t - s * kvec;
-  const int64_t p0 = s * rows_per_slab;
-  int64_t p1 = p0 + rows_per_slab;
-  p1 = p1 < P ? p1 : P;
-  uint32_t m[N];
-#pragma unroll
-  for (int j = 0; j < N; ++j) m[j] = 0;
-  for (int64_t p = p0; p < p1; ++p) {
-    V v = ldg_vec(x + p * K + kv * N);
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      uint32_t b = abs_bits_t<T>(v.e[j]);
-      m[j] = b > m[j] ? b : m[j];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < N; ++j) atomicMax(out + kv * N + j, m[j]);
 }
 
 // Generic: one element per lane, atomicMax per element (any P, K, Q, alignment).
@@ -959,14 +837,6 @@ __global__ __launch_bounds__(kThreads) void amax_generic_kernel(const T *__restr
     int64_t k = (i / Q) % K;
     atomicMax(out + k, abs_bits_t<T>(x[i]));
   }
-}
-
-int env_variant(const char *name, int *cache) {
-  if (*cache < 0) {
-    const char *e = getenv(name);
-    *cache = e ? atoi(e) : 0;
-  }
-  return *cache;
 }
 
 // Rows, unrolled form: one item = (row, chunk of <= G*U vectors) per group of G lanes, U
@@ -1012,78 +882,6 @@ __global__ __launch_bounds__(kThreads) void amax_rows_u_kernel(const T *__restri
     } else {
       atomicMax(out + (r % K), m);
     }
-  }
-}
-
-// Columns, LDS form: x viewed as [P, K] (K % N == 0); a block owns a chunk of `lpr` column
-// vectors (lpr <= kThreads lanes across a row, kThreads / lpr row lanes) and a slab of rows,
-// keeps U loads in flight per lane, folds its row lanes in LDS and issues one atomicMax per
-// column.  The old form (one slab per lane, N atomics per lane) spent most of its time in
-// ~2 M same-address atomics at [32768, 4096].
-template <typename T, int U>
-__global__ __launch_bounds__(kThreads) void amax_cols_lds_kernel(const T *__restrict__ x,
-                                                                  int64_t P, int64_t K, int lpr,
-                                                                  int64_t nchunks,
-                                                                  int64_t rows_per_slab,
-                                                                  uint32_t *out) {
-  using V = Vec<T>;
-  constexpr int N = V::N;
-  __shared__ uint32_t sh[kThreads * N];
-  const int64_t kvec = K / N;
-  const int64_t chunk = blockIdx.x % nchunks, slab = blockIdx.x / nchunks;
-  const int tc = threadIdx.x % lpr, tr = threadIdx.x / lpr;
-  const int rstep = kThreads / lpr;
-  const int64_t kv = chunk * lpr + tc;
-  const bool active = tr < rstep && kv < kvec;
-  if (rstep > 1) {
-    for (int i = threadIdx.x; i < lpr * N; i += kThreads) sh[i] = 0;
-    __syncthreads();
-  }
-  uint32_t m[N];
-#pragma unroll
-  for (int j = 0; j < N; ++j) m[j] = 0;
-  if (active) {
-    const int64_t p0 = slab * rows_per_slab;
-    int64_t p1 = p0 + rows_per_slab;
-    p1 = p1 < P ? p1 : P;
-    const T *base = x + kv * N;
-    int64_t p = p0 + tr;
-    for (; p + (int64_t)(U - 1) * rstep < p1; p += (int64_t)U * rstep) {
-      V v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ldg_vec_nt(base + (p + (int64_t)u * rstep) * K);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          uint32_t b = abs_bits_t<T>(v[u].e[j]);
-          m[j] = b > m[j] ? b : m[j];
-        }
-    }
-    for (; p < p1; p += rstep) {
-      V v = ldg_vec_nt(base + p * K);
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        uint32_t b = abs_bits_t<T>(v.e[j]);
-        m[j] = b > m[j] ? b : m[j];
-      }
-    }
-  }
-  if (rstep == 1) {
-    if (active)
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-        if (m[j]) atomicMax(out + kv * N + j, m[j]);
-    return;
-  }
-  if (active)
-#pragma unroll
-    for (int j = 0; j < N; ++j)
-      if (m[j]) atomicMax(sh + tc * N + j, m[j]);
-  __syncthreads();
-  for (int i = threadIdx.x; i < lpr * N; i += kThreads) {
-    const int64_t col = chunk * lpr * N + i;
-    if (col < K && sh[i]) atomicMax(out + col, sh[i]);
   }
 }
 
@@ -1253,27 +1051,6 @@ int launch_amax_rows_u(const T *x, int64_t P, int64_t K, int64_t Q, uint32_t *ou
 }
 
 template <typename T>
-int launch_amax_cols_lds(const T *x, int64_t P, int64_t K, uint32_t *out, int blocks_per_cu,
-                         hipStream_t stream) {
-  constexpr int N = Vec<T>::N, U = 8;
-  const int64_t kvec = K / N;
-  const int lpr = (int)(kvec < kThreads ? kvec : kThreads);
-  const int64_t nchunks = (kvec + lpr - 1) / lpr;
-  const int rstep = kThreads / lpr;
-  const int64_t want = (int64_t)num_cus() * blocks_per_cu;
-  int64_t slabs = (want + nchunks - 1) / nchunks;
-  // at least U row steps per slab so the unrolled body runs
-  const int64_t max_slabs = (P + (int64_t)U * rstep - 1) / ((int64_t)U * rstep);
-  if (slabs > max_slabs) slabs = max_slabs;
-  if (slabs < 1) slabs = 1;
-  const int64_t rows_per_slab = (P + slabs - 1) / slabs;
-  slabs = (P + rows_per_slab - 1) / rows_per_slab;
-  const unsigned g = (unsigned)(nchunks * slabs);
-  amax_cols_lds_kernel<T, U><<<g, kThreads, 0, stream>>>(x, P, K, lpr, nchunks, rows_per_slab, out);
-  return check_launch();
-}
-
-template <typename T>
 int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
                 hipStream_t stream) {
   const T *x = reinterpret_cast<const T *>(xv);
@@ -1283,78 +1060,19 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
   constexpr int N = Vec<T>::N;
   const bool al = aligned16(x);
   if (K == 1 && (Q == 1 || P == 1)) {  // per-tensor
-    int64_t nvec = al ? n / N : 0;
-    switch (al ? amax_variant() : 1) {  // unaligned: all-scalar grid-stride form
-    case 1: {
+    if (!al) {  // unaligned: the all-scalar grid-stride form
       unsigned g = grid_for(n / N + 1, kThreads * 4);
-      amax_all_kernel<T><<<g, kThreads, 0, stream>>>(x, n, nvec, out);
+      amax_all_kernel<T><<<g, kThreads, 0, stream>>>(x, n, 0, out);
       return check_launch();
     }
-    case 2:
-      return launch_amax_persist<T, 8>(x, n, nvec, out, 1, stream);
-    case 3:
-      return launch_amax_persist<T, 8>(x, n, nvec, out, 4, stream);
-    case 4:
-      return launch_amax_persist<T, 4>(x, n, nvec, out, 2, stream);
-    default:
-      return launch_amax_persist<T, 8>(x, n, nvec, out, 2, stream);
-    }
+    // persistent grid, 2 x 1024-thread blocks per CU, 8 loads in flight per lane (r01 sweep,
+    // scripts/sweep_amax.py: 1 / 4 blocks per CU or 4 loads per lane no faster)
+    return launch_amax_persist<T, 8>(x, n, n / N, out, 2, stream);
   }
-  static int rows_v = -1, cols_v = -1;
-  if (Q % N == 0 && al && Q >= N && env_variant("MTQ_AMD_ROWS_VARIANT", &rows_v) != 1)
-    return launch_amax_rows_u<T>(x, P, K, Q, out, stream);
-  if (Q == 1 && K % N == 0 && al && env_variant("MTQ_AMD_COLS_VARIANT", &cols_v) != 1) {
-    switch (cols_v) {
-    case 2:
-      return launch_amax_cols_lds<T>(x, P, K, out, 2, stream);
-    case 3:
-      return launch_amax_cols_wide<T>(x, P, K, out, 4, stream);
-    case 4:
-      return launch_amax_cols_wide<T>(x, P, K, out, 1, stream);
-    case 5:
-      return launch_amax_cols_wide<T>(x, P, K, out, 2, stream);
-    default:
-      return launch_amax_cols_wide<T>(x, P, K, out, 0, stream);
-    }
-  }
-  if (Q % N == 0 && al && Q >= N) {
-    const int64_t R = P * K, qvec = Q / N;
-    // chunk long rows so that there are enough independent items to fill the chip
-    int64_t chunk_vec = qvec;
-    const int64_t want_items = (int64_t)num_cus() * 16;
-    if (R < want_items && qvec > 512) {
-      int64_t chunks = (want_items + R - 1) / R;
-      chunk_vec = (qvec + chunks - 1) / chunks;
-      chunk_vec = (chunk_vec + 63) / 64 * 64;
-    }
-    int64_t chunks = (qvec + chunk_vec - 1) / chunk_vec;
-    int64_t items = R * chunks;
-    if (chunk_vec >= 64) {
-      unsigned g = grid_for(items, kThreads / 64);
-      amax_rows_kernel<T, 64><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunk_vec, chunks, out);
-    } else if (chunk_vec >= 16) {
-      unsigned g = grid_for(items, kThreads / 16);
-      amax_rows_kernel<T, 16><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunk_vec, chunks, out);
-    } else {
-      unsigned g = grid_for(items, kThreads / 4);
-      amax_rows_kernel<T, 4><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunk_vec, chunks, out);
-    }
-    return check_launch();
-  }
-  if (Q == 1 && K % N == 0 && al) {
-    const int64_t kvec = K / N;
-    // enough slabs for ~16 waves per CU
-    int64_t want_threads = (int64_t)num_cus() * kThreads * 4;
-    int64_t slabs = (want_threads + kvec - 1) / kvec;
-    if (slabs > P) slabs = P;
-    if (slabs < 1) slabs = 1;
-    int64_t rows_per_slab = (P + slabs - 1) / slabs;
-    slabs = (P + rows_per_slab - 1) / rows_per_slab;
-    int64_t threads = kvec * slabs;
-    unsigned g = (unsigned)((threads + kThreads - 1) / kThreads);
-    amax_cols_kernel<T><<<g, kThreads, 0, stream>>>(x, P, K, rows_per_slab, out);
-    return check_launch();
-  }
+  if (Q % N == 0 && al && Q >= N) return launch_amax_rows_u<T>(x, P, K, Q, out, stream);
+  // per-column (axis -1 kept): 1024-thread wide-column kernel with the LDS fold; the block count
+  // per CU is picked from the shape (launch_amax_cols_wide)
+  if (Q == 1 && K % N == 0 && al) return launch_amax_cols_wide<T>(x, P, K, out, 0, stream);
   unsigned g = grid_for(n, kThreads);
   amax_generic_kernel<T><<<g, kThreads, 0, stream>>>(x, n, K, Q, out);
   return check_launch();
@@ -1363,7 +1081,7 @@ int launch_amax(const void *xv, int64_t P, int64_t K, int64_t Q, float *outf,
 // ============================================================================================
 // Dynamic INT-n block quant with optional per-column pre-quant scale (AWQ-lite weight side)
 // ============================================================================================
-// U vectors per lane (MTQ_AMD_BQD_U = 1 or 2, default 2): all U loads issued first
+// U vectors per lane, all U loads issued first
 template <typename T, int BLK, int U>
 __global__ __launch_bounds__(kThreads) void block_quant_dyn_kernel(
     const T *__restrict__ x, T *__restrict__ y, const T *__restrict__ pqs, int64_t nvec,
@@ -1430,41 +1148,6 @@ __global__ __launch_bounds__(kThreads) void hist_kernel(const T *__restrict__ x,
     for (int b = threadIdx.x; b < bins; b += kThreads)
       if (sh[b]) atomicAdd(counts + b, sh[b]);
   }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kThreads) void hist_vec_kernel(const T *__restrict__ x,
-                                                             int64_t nvec, const float *hmax,
-                                                             int bins, int skip_zeros,
-                                                             uint32_t *counts) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
-  using V = Vec<T>;
-  float lo = 0.f, hi = *hmax;
-  if (hi == lo) {
-    lo -= 1.f;
-    hi += 1.f;
-  }
-  const float fb = (float)bins;
-  const float span = hi - lo;
-  for (int b = threadIdx.x; b < bins; b += kThreads) sh[b] = 0;
-  __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride) {
-    V v = ldg_vec(x + i * V::N);
-#pragma unroll
-    for (int j = 0; j < V::N; ++j) {
-      float a = fabsf(Elem<T>::ld(v.e[j]));
-      bool ok = (a >= lo && a <= hi) && !(skip_zeros && a == 0.f);
-      if (ok) {
-        int b = (int)(((a - lo) * fb) / span);
-        if (b == bins) b -= 1;
-        atomicAdd(sh + b, 1u);
-      }
-    }
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < bins; b += kThreads)
-    if (sh[b]) atomicAdd(counts + b, sh[b]);
 }
 
 // Division form (default, any dtype): the per-element true division of the formula above is
@@ -1801,52 +1484,9 @@ __global__ __launch_bounds__(kThreads) void nvfp4_vec_kernel(const T *__restrict
 // and widened back by one v_cvt_scalef32_pk_f32_fp4, times q.  Symmetric rounding makes the
 // signed form equal to the reference's sign(x) * e2m1(|x| / q) * q except for x = -0 and NaN
 // (mtq_device.hpp Fp4Native): blocks with a NaN and lanes with a -0 take nvfp4_qdq.
-template <typename T, int BS>
-__global__ __launch_bounds__(kThreads) void nvfp4_native_kernel(const T *__restrict__ x,
-                                                                 T *__restrict__ y, int64_t nvec,
-                                                                 const float *__restrict__ gamax) {
-  using V = Vec<T>;
-  constexpr int N = V::N;
-  static_assert(N == 8 && BS % N == 0, "16-bit elements, block a multiple of the vector");
-  constexpr int LPB = BS / N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i - (threadIdx.x % LPB) >= nvec) return;
-  const float gs = nvfp4_global_scale(gamax);
-  V v = ldg_vec_nt(x + i * N);
-  uint32_t w[4] = {v.raw.x, v.raw.y, v.raw.z, v.raw.w};
-  const PairScan sc = scan_pairs(w);
-  const uint32_t mb = group_max_u32<LPB>(sc.max_abs);
-  const bool block_nan = mb > Fp4Native<T>::kInfBits;
-  float bmax;
-  if (!block_nan) {
-    bmax = half_bits_to_float<T>(mb);
-  } else {  // NaN skipped (max.f32 under the reference's Triton tl.max), as nvfp4_vec_kernel
-    float m = 0.f;
-#pragma unroll
-    for (int j = 0; j < N; ++j) m = max_skip_nan(m, fabsf(Elem<T>::ld(v.e[j])));
-    bmax = group_max_f<LPB>(m);
-  }
-  const Nvfp4Block b = nvfp4_block(bmax, gs);
-  if (!block_nan && !sc.neg_zero) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float a0 = div_rn(Elem<T>::ld(v.e[2 * j]), b.q, b.r);
-      const float a1 = div_rn(Elem<T>::ld(v.e[2 * j + 1]), b.q, b.r);
-      const uint32_t c = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, a0, a1, 1.0f, 0);
-      const auto r = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(c, 1.0f, 0);
-      v.e[2 * j] = Elem<T>::st(r[0] * b.q);
-      v.e[2 * j + 1] = Elem<T>::st(r[1] * b.q);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < N; ++j) v.e[j] = Elem<T>::st(nvfp4_qdq(Elem<T>::ld(v.e[j]), b));
-  }
-  stg_vec_nt(y + i * N, v);
-}
-
-// U vectors per lane (MTQ_AMD_NVFP4_U, default 2; 1 = nvfp4_native_kernel above): all U loads
-// issued before the first block is converted, and the per-thread constants (global scale, its
-// 6x reciprocal) paid once per U vectors.  Each u-slice is exactly nvfp4_native_kernel's body.
+// U = 2 vectors per lane, both loads issued before the first block is converted, the per-thread
+// constants (global scale, its 6x reciprocal) paid once per U vectors: 0.755-0.760 -> 0.772-0.774
+// of the HBM roofline over one vector per lane, U = 4 slower (profiles/r03/nvfp4).
 template <typename T, int BS, int U>
 __global__ __launch_bounds__(kThreads) void nvfp4_native_u_kernel(const T *__restrict__ x,
                                                                    T *__restrict__ y, int64_t nvec,
@@ -1928,22 +1568,9 @@ int launch_nvfp4(const T *x, T *y, int64_t rows, int64_t cols, const float *gama
     const int64_t nvec = rows * cols / N;
     const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
     if constexpr (sizeof(T) == 2) {
-      static int nv = -1;  // MTQ_AMD_FP4_EMULATE=1 forces the table emulation (A/B runs)
-      if (env_variant("MTQ_AMD_FP4_EMULATE", &nv) == 0) {
-        static int nu = -1;  // MTQ_AMD_NVFP4_U: vectors per lane (1, 2 or 4; default 2)
-        if (nu < 0) {
-          const char *e = getenv("MTQ_AMD_NVFP4_U");
-          nu = e ? atoi(e) : 2;
-          if (nu != 1 && nu != 2 && nu != 4) nu = 2;
-        }
-        if (nu == 1)
-          nvfp4_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec, gamax);
-        else if (nu == 2)
-          nvfp4_native_u_kernel<T, BS, 2><<<(unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0, stream>>>(x, y, nvec, gamax);
-        else
-          nvfp4_native_u_kernel<T, BS, 4><<<(unsigned)((nvec + 4 * kThreads - 1) / (4 * kThreads)), kThreads, 0, stream>>>(x, y, nvec, gamax);
-        return check_launch();
-      }
+      nvfp4_native_u_kernel<T, BS, 2><<<(unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0,
+                                        stream>>>(x, y, nvec, gamax);
+      return check_launch();
     }
     nvfp4_vec_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec, gamax);
   } else {
@@ -2183,8 +1810,8 @@ __device__ __forceinline__ int64_t idx_div(int64_t n, int64_t d, const FastDiv &
     return n / d;
 }
 
-// Native fast paths of the packers (`native` kernel argument, MTQ_AMD_EXPORT_NATIVE=0 turns them
-// off for A/B): each lane first converts its vector with the gfx950 converts and a handful of
+// Native fast paths of the packers (`native` kernel argument, always 1 from the launchers; 0 =
+// the emulated conversions only, the r01 packers): each lane first converts its vector with the gfx950 converts and a handful of
 // VALU ops, checks the few inputs where the converter and the reference disagree, and only a lane
 // that holds one of those redoes the vector on the exact emulated path above.  The emulated path
 // costs ~25 VALU ops per element (seven threshold compares per E2M1 code), which made the packers
@@ -2581,7 +2208,6 @@ __global__ __launch_bounds__(kThreads) void export_fp8_pt_kernel(const T *__rest
     if (base + u * kThreads < nvec) export_fp8_pt_one<T, ROUND>(base + u * kThreads, v[u], y, s, r);
 }
 
-// U consecutive 256-vector chunks per block (MTQ_AMD_EXPORT_U = 1, 2 or 4; default 2).
 template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__restrict__ x,
                                                                    uint8_t *__restrict__ y,
@@ -2632,43 +2258,9 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
   for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK>(base + u * kThreads, x, y, sc, nvec, native);
 }
 
-int export_u() {
-  static int u = -1;
-  if (u < 0) {
-    const char *e = getenv("MTQ_AMD_EXPORT_U");
-    u = e ? atoi(e) : 2;
-    if (u != 1 && u != 2 && u != 4) u = 2;
-  }
-  return u;
-}
-// calls f(std::integral_constant<int, U>) with the configured U
-template <class F> void with_export_u(F &&f) {
-  const int u = export_u();
-  if (u == 4)
-    f(std::integral_constant<int, 4>{});
-  else if (u == 1)
-    f(std::integral_constant<int, 1>{});
-  else
-    f(std::integral_constant<int, 2>{});
-}
-// MTQ_AMD_EXPORT_NATIVE=0: emulated conversions only (A/B of the native fast paths)
-int export_native() {
-  static int n = -1;
-  if (n < 0) {
-    const char *e = getenv("MTQ_AMD_EXPORT_NATIVE");
-    n = e ? (atoi(e) != 0) : 1;
-  }
-  return n;
-}
-// MTQ_AMD_EXPORT_FP8_PT=0: per-tensor FP8 export through the generic kernel (A/B)
-int export_fp8_pt() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("MTQ_AMD_EXPORT_FP8_PT");
-    v = e ? (atoi(e) != 0) : 1;
-  }
-  return v;
-}
+// U = 2 consecutive 256-vector chunks per block (U = 1 / 4 within run-to-run noise,
+// profiles/r02/export/export_u_ab.json)
+template <class F> void with_export_u(F &&f) { f(std::integral_constant<int, 2>{}); }
 unsigned export_grid(int64_t nvec, int u) { return (unsigned)((nvec + kThreads * u - 1) / (kThreads * u)); }
 
 // MXFP8QTensor.quantize (qtensor/mxfp8_tensor.py:36-52 + 163-187): per 32-block along the rows,
@@ -2858,21 +2450,12 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
     const T *xt = reinterpret_cast<const T *>(x);
     T *yt = reinterpret_cast<T *>(y);
     const T *pt = reinterpret_cast<const T *>(pqs);
-    static int bu = -1;  // MTQ_AMD_BQD_U: vectors per lane (1 or 2; default 2)
-    if (bu < 0) {
-      const char *e = getenv("MTQ_AMD_BQD_U");
-      bu = (e && atoi(e) == 1) ? 1 : 2;
-    }
-    auto go = [&](auto blk_c, auto u_c) {
-      constexpr int BLK = decltype(blk_c)::value, U = decltype(u_c)::value;
+    // U = 2 vectors per lane, both loads first: 0.738 -> 0.766 of the HBM roofline over one
+    // (profiles/r03/dyn_u/)
+    auto go_u = [&](auto blk_c) {
+      constexpr int BLK = decltype(blk_c)::value, U = 2;
       const unsigned gu = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
       block_quant_dyn_kernel<T, BLK, U><<<gu, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
-    };
-    auto go_u = [&](auto blk_c) {
-      if (bu == 1)
-        go(blk_c, std::integral_constant<int, 1>{});
-      else
-        go(blk_c, std::integral_constant<int, 2>{});
     };
     switch (block) {
     case 32: go_u(std::integral_constant<int, 32>{}); break;
@@ -2900,14 +2483,11 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
     const T *xt = reinterpret_cast<const T *>(x);
     const bool lds = bins <= 16384;
     const size_t shm = lds ? (size_t)bins * 4 : 0;
-    static int hv = -1;
-    const int var = env_variant("MTQ_AMD_HIST_VARIANT", &hv);
-    // 16-bit dtypes: pattern histogram + per-block fold.  Variants measured on bf16
-    // [32768, 4096], 2048 bins (profiles/r02/histogram/): 0 = U 2 with register prefetch
-    // 46.9 us (71.6 %); 20 = U 4 no prefetch 48.4; 21 = U 4 prefetch 49.6; 22 = U 8 prefetch
-    // 54.1; 23 = U 1 prefetch 56.5; 24 = U 2 no prefetch 46.8-47.3.
+    // 16-bit dtypes: pattern histogram + per-block fold, U = 2 vectors per lane with a register
+    // prefetch (bf16 [32768, 4096], 2048 bins: 46.9 us = 71.6 %; U 1 / 4 / 8 and no prefetch
+    // measured no faster, profiles/r02/histogram/).
     if constexpr (sizeof(T) == 2) {
-      if ((var == 0 || (var >= 20 && var <= 24)) && aligned16(x) && n % N == 0 && bins <= 8192) {
+      if (aligned16(x) && n % N == 0 && bins <= 8192) {
         const int64_t nvec = n / N;
         int64_t blocks = num_cus();
         const int64_t min_per_block = (int64_t)kHistValThreads * 8;
@@ -2915,46 +2495,31 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
         vpb = vpb < min_per_block ? min_per_block : vpb;
         blocks = (nvec + vpb - 1) / vpb;
         const size_t shr = ((size_t)kHistPatterns + (size_t)bins) * 4;
-        auto go = [&](auto kern, int slot) {
-          static bool attr[6] = {false, false, false, false, false, false};  // per kernel
-          if (!attr[slot]) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr[slot] = true;
-          }
-          kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins,
-                                                                   skip_zeros, counts);
-          return check_launch();
-        };
-        if (var == 20) return go(hist_value_kernel<T, 4, false>, 1);
-        if (var == 21) return go(hist_value_kernel<T, 4, true>, 2);
-        if (var == 22) return go(hist_value_kernel<T, 8, true>, 3);
-        if (var == 23) return go(hist_value_kernel<T, 1, true>, 4);
-        if (var == 24) return go(hist_value_kernel<T, 2, false>, 5);
-        return go(hist_value_kernel<T, 2, true>, 0);
+        auto kern = hist_value_kernel<T, 2, true>;
+        static bool attr = false;
+        if (!attr) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          attr = true;
+        }
+        kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        return check_launch();
       }
     }
-    // variants (MTQ_AMD_HIST_VARIANT, scripts/sweep_reduce.py): 0 = REP 4, 2 blocks per CU
-    // (4.3 TB/s on bf16 [32768, 4096]); 8 = REP 8, 1 block per CU; 9 = REP 8, 2 per CU;
-    // 1 = the plain LDS-privatised kernels below (2.4 TB/s, VALU-bound on the division)
-    // (10 = the REP-4 division kernel for 16-bit dtypes too; fp32 and > 8192 bins land here)
-    if ((var == 0 || var == 8 || var == 9 || var == 10 || var == 20) && aligned16(x) &&
-        n % N == 0 && bins <= 16384) {
-      int rep = (var == 8 || var == 9) ? 8 : 4;
+    // fp32 (and > 8192 bins): REP interleaved LDS copies of the bins (REP 4 while bins * REP fits
+    // 16384 words), 2 blocks per CU (scripts/sweep_reduce.py: 4.3 TB/s on bf16 [32768, 4096]
+    // against 2.4 TB/s for one copy; REP 8 / 1 block per CU no faster)
+    if (aligned16(x) && n % N == 0 && lds) {
+      int rep = 4;
       while (rep > 1 && (int64_t)bins * rep > 16384) rep >>= 1;
-      const int per_cu = var == 8 ? 1 : 2;
       const int64_t nvec = n / N;
-      int64_t blocks = (int64_t)num_cus() * per_cu;
+      int64_t blocks = (int64_t)num_cus() * 2;
       const int64_t min_per_block = (int64_t)kHistDivThreads * 8;
       int64_t vpb = (nvec + blocks - 1) / blocks;
       vpb = vpb < min_per_block ? min_per_block : vpb;
       blocks = (nvec + vpb - 1) / vpb;
       const size_t shr = (size_t)bins * rep * 4;
       switch (rep) {
-      case 8:
-        hist_div_kernel<T, 8, 4><<<(unsigned)blocks, kHistDivThreads, shr, stream>>>(
-            xt, nvec, vpb, hmax, bins, skip_zeros, counts);
-        break;
       case 4:
         hist_div_kernel<T, 4, 4><<<(unsigned)blocks, kHistDivThreads, shr, stream>>>(
             xt, nvec, vpb, hmax, bins, skip_zeros, counts);
@@ -2969,14 +2534,9 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
       }
       return check_launch();
     }
-    if (lds && aligned16(x) && n % N == 0) {
-      unsigned g = grid_for(n / N, kThreads * 8);
-      hist_vec_kernel<T><<<g, kThreads, shm, stream>>>(xt, n / N, hmax, bins, skip_zeros, counts);
-    } else {
-      unsigned g = grid_for(n, kThreads * 8);
-      hist_kernel<T><<<g, kThreads, shm, stream>>>(xt, n, hmax, bins, skip_zeros, counts,
-                                                   lds ? 1 : 0);
-    }
+    // unaligned / ragged inputs, or bins past the LDS: one element per lane
+    unsigned g = grid_for(n, kThreads * 8);
+    hist_kernel<T><<<g, kThreads, shm, stream>>>(xt, n, hmax, bins, skip_zeros, counts, lds ? 1 : 0);
     return check_launch();
   });
 }
@@ -3074,7 +2634,7 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
     if (cols % N == 0 && aligned16(x) && ((uintptr_t)y % N) == 0) {
       const int64_t nvec = n / N, cv = cols / N;
       const FastDiv fcv = make_fastdiv(cv < (1ll << 31) ? (uint32_t)cv : 1u);
-      if (!per_row && export_native() && export_fp8_pt())
+      if (!per_row)
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           if (round_to_dtype)
@@ -3088,13 +2648,13 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_fp8_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype, export_native());
+            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype, 1);
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_fp8_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype, export_native());
+            reinterpret_cast<const T *>(x), y, nvec, cv, fcv, scale, per_row, round_to_dtype, 1);
         });
     } else {
       export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
@@ -3155,13 +2715,13 @@ int mtq_export_nvfp4(const void *x, uint8_t *y, int64_t rows, int64_t cols, int 
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_nvfp4_vec_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2, export_native());
+            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2, 1);
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_nvfp4_vec_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2, export_native());
+            reinterpret_cast<const T *>(x), y, nvec, vpb, fvpb, block_scale, scale_2, 1);
         });
     } else {
       export_nvfp4_kernel<T><<<grid_for(npairs, kThreads), kThreads, 0, stream>>>(
@@ -3200,12 +2760,12 @@ int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int 
       if (block == 32)
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
-          export_mxfp4_vec_kernel<U, T, 32><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, export_native());
+          export_mxfp4_vec_kernel<U, T, 32><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
-          export_mxfp4_vec_kernel<U, T, 16><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, export_native());
+          export_mxfp4_vec_kernel<U, T, 16><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
         });
     } else {
       export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(

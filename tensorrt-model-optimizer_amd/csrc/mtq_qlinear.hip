@@ -163,10 +163,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, ui
 
 // PT: per-tensor amax.  SPB: 0 = amax blocks hold a whole number of U-step batches (one amax per
 // batch per lane), else K steps per amax block (SPB divides U: U / SPB amax per batch).
-// PROBE (measurement builds, MTQ_AMD_QLINEAR_PROBE): 1 = raw W to the MFMA (no qdq), 2 = loads
-// only (the W bits folded into the accumulator), 3 = loads only with 1 KB-contiguous W
-// instructions (same bytes), 4 = W loads only (no x loads)
-template <typename T, int KIND, int U, bool PT, int SPB, int PROBE = 0>
+template <typename T, int KIND, int U, bool PT, int SPB>
 __global__ __launch_bounds__(kStreamWaves * 64) void qlinear_stream_kernel(
     const T *__restrict__ x, const T *__restrict__ w, T *__restrict__ y, const T *__restrict__ bias,
     float *__restrict__ part, int M, int N, int K, int tiles, int S, int kcs, QlParams p) {
@@ -204,14 +201,8 @@ __global__ __launch_bounds__(kStreamWaves * 64) void qlinear_stream_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int st = s + u < s1 ? s + u : s1 - 1;  // scalar clamp: the tail re-reads a valid step
-      if (PROBE == 3)  // same bytes per step, 1 KB contiguous per instruction
-        wv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, lane * 16, st * 1024, 2));
-      else
-        wv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, wlane, st * 64, 2));
-      if (PROBE != 4)  // 4: no x loads
-        xv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xlane, st * 64, 0));
-      else
-        xv[u] = u32x4{(uint32_t)st, 0u, 0u, 0u};
+      wv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, wlane, st * 64, 2));
+      xv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xlane, st * 64, 0));
     }
     if constexpr (NA > 0) {
 #pragma unroll
@@ -242,18 +233,11 @@ __global__ __launch_bounds__(kStreamWaves * 64) void qlinear_stream_kernel(
       if (s + u >= s1) break;  // wave-uniform
       if (SPB > 0 && u % (SPB > 0 ? SPB : 1) == 0) qp.make(av[u / (SPB > 0 ? SPB : 1)], p);
       u32x4 b;
-      if (PROBE == 0) {
-        b.x = qp.template pair<T>(wv[u].x);
-        b.y = qp.template pair<T>(wv[u].y);
-        b.z = qp.template pair<T>(wv[u].z);
-        b.w = qp.template pair<T>(wv[u].w);
-      } else {
-        b = wv[u];
-      }
-      if (PROBE >= 2)
-        acc[0] += __uint_as_float(b.x ^ b.y ^ b.z ^ b.w ^ xv[u].x);
-      else
-        acc = Mfma<T>::mma(as_v8<T>(xv[u]), as_v8<T>(b), acc);
+      b.x = qp.template pair<T>(wv[u].x);
+      b.y = qp.template pair<T>(wv[u].y);
+      b.z = qp.template pair<T>(wv[u].z);
+      b.w = qp.template pair<T>(wv[u].w);
+      acc = Mfma<T>::mma(as_v8<T>(xv[u]), as_v8<T>(b), acc);
     }
   };
 
@@ -334,17 +318,15 @@ template <int XM> struct XLayout {
   static constexpr int ring = 2;
 };
 
-// PROBE (measurement builds): 1 = raw W to the MFMA, 2 = no qdq and no MFMA (the slot's bits
-// folded into the accumulator); RING overrides the ring depth (0: XLayout's)
 // One unit (16-row tile x K chunk) of one linear; `unit` and `wave` wave-uniform.
-template <typename T, int KIND, bool PT, int XM, int PROBE = 0, int RING = 0>
+template <typename T, int KIND, bool PT, int XM>
 __device__ __forceinline__ void qlinear_dma_unit(
     const T *__restrict__ x, const T *__restrict__ w, T *__restrict__ y, const T *__restrict__ bias,
     float *__restrict__ part, int M, int N, int K, int tiles, int S, int kcs, const QlParams &p,
     int unit, int wave) {
   constexpr int U = 4;
   using XL = XLayout<XM>;
-  constexpr int R = RING ? RING : XL::ring, SLOT = XL::slot;
+  constexpr int R = XL::ring, SLOT = XL::slot;
   constexpr int GROUP = 4 + XL::dmas + (PT ? 0 : 1);  // DMA instructions per batch
   __shared__ __attribute__((aligned(16))) unsigned char lds[kStreamWaves * R * SLOT];
   const int lane = threadIdx.x & 63;
@@ -456,17 +438,12 @@ __device__ __forceinline__ void qlinear_dma_unit(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (s + u >= s1) break;  // wave-uniform
-      u32x4 bq = wf[u];
-      if (PROBE == 0) {
-        bq.x = qp.template pair<T>(wf[u].x);
-        bq.y = qp.template pair<T>(wf[u].y);
-        bq.z = qp.template pair<T>(wf[u].z);
-        bq.w = qp.template pair<T>(wf[u].w);
-      }
-      if (PROBE == 2)
-        acc[0] += __uint_as_float(bq.x ^ bq.y ^ bq.z ^ bq.w ^ xf[u].x);
-      else
-        acc = Mfma<T>::mma(as_v8<T>(xf[u]), as_v8<T>(bq), acc);
+      u32x4 bq;
+      bq.x = qp.template pair<T>(wf[u].x);
+      bq.y = qp.template pair<T>(wf[u].y);
+      bq.z = qp.template pair<T>(wf[u].z);
+      bq.w = qp.template pair<T>(wf[u].w);
+      acc = Mfma<T>::mma(as_v8<T>(xf[u]), as_v8<T>(bq), acc);
     }
   };
 
@@ -498,14 +475,14 @@ __device__ __forceinline__ void qlinear_dma_unit(
   }
 }
 
-template <typename T, int KIND, bool PT, int XM, int PROBE = 0, int RING = 0>
+template <typename T, int KIND, bool PT, int XM>
 __global__ __launch_bounds__(kStreamWaves * 64) void qlinear_dma_kernel(
     const T *__restrict__ x, const T *__restrict__ w, T *__restrict__ y, const T *__restrict__ bias,
     float *__restrict__ part, int M, int N, int K, int tiles, int S, int kcs, QlParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int unit = __builtin_amdgcn_readfirstlane(blockIdx.x * kStreamWaves) + wave;
   if (unit >= tiles * S) return;  // wave-uniform; the kernel has no barrier
-  qlinear_dma_unit<T, KIND, PT, XM, PROBE, RING>(x, w, y, bias, part, M, N, K, tiles, S, kcs, p, unit, wave);
+  qlinear_dma_unit<T, KIND, PT, XM>(x, w, y, bias, part, M, N, K, tiles, S, kcs, p, unit, wave);
 }
 
 // Several linears of the same input length M and depth K in one launch (the q/k/v projections of
@@ -667,21 +644,8 @@ __global__ __launch_bounds__(kQlWaves * 64) void qlinear_wg_kernel(
 // ---- host ----------------------------------------------------------------------------------
 constexpr int kU = 4;  // K steps per batch (4 x 16 B of W per lane in flight, double-buffered)
 
-int env_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// waves a launch aims for: split K until tiles x S reaches it (MTQ_AMD_QLINEAR_WAVES overrides;
-// default 8 per CU, two per SIMD)
-int64_t target_waves() {
-  static int64_t t = -1;
-  if (t < 0) {
-    t = env_int("MTQ_AMD_QLINEAR_WAVES", 0);
-    if (t <= 0) t = 8 * (int64_t)mtq::host_num_cus();
-  }
-  return t;
-}
+// waves a launch aims for: split K until tiles x S reaches it (8 per CU, two per SIMD)
+int64_t target_waves() { return 8 * (int64_t)mtq::host_num_cus(); }
 
 struct Split {
   int S, kcs;
@@ -715,23 +679,6 @@ int stream_spb(int64_t amax_numel, int64_t block, int64_t K) {
 template <typename T, int KIND, int XM>
 void launch_dma(unsigned g, bool pt, hipStream_t stream, const T *x, const T *w, T *y, const T *bias,
                 float *part, int M, int N, int K, int tiles, int S, int kcs, const QlParams &p) {
-  static const int probe = env_int("MTQ_AMD_QLINEAR_PROBE", 0);
-  static const int ring = env_int("MTQ_AMD_QLINEAR_RING", 0);
-  if (XM == 1 && pt && (probe || ring)) {  // measurement variants
-    if (probe == 1)
-      qlinear_dma_kernel<T, KIND, true, XM, 1><<<g, kStreamWaves * 64, 0, stream>>>(x, w, y, bias, part, M, N, K,
-                                                                                   tiles, S, kcs, p);
-    else if (probe == 2)
-      qlinear_dma_kernel<T, KIND, true, XM, 2><<<g, kStreamWaves * 64, 0, stream>>>(x, w, y, bias, part, M, N, K,
-                                                                                   tiles, S, kcs, p);
-    else if (ring == 2)
-      qlinear_dma_kernel<T, KIND, true, XM, 0, 2><<<g, kStreamWaves * 64, 0, stream>>>(x, w, y, bias, part, M, N,
-                                                                                      K, tiles, S, kcs, p);
-    else
-      qlinear_dma_kernel<T, KIND, true, XM, 0, 3><<<g, kStreamWaves * 64, 0, stream>>>(x, w, y, bias, part, M, N,
-                                                                                      K, tiles, S, kcs, p);
-    return;
-  }
   if (pt)
     qlinear_dma_kernel<T, KIND, true, XM><<<g, kStreamWaves * 64, 0, stream>>>(x, w, y, bias, part, M, N, K,
                                                                               tiles, S, kcs, p);
@@ -751,9 +698,7 @@ int launch_stream(const void *x, const void *w, const void *bias, void *y, float
   T *yt = reinterpret_cast<T *>(y);
   const bool pt = p.amax_numel == 1;
 #define QL_ARGS xt, wt, yt, bt, part, (int)M, (int)N, (int)K, tiles, sp.S, sp.kcs, p
-  static const int probe = env_int("MTQ_AMD_QLINEAR_PROBE", 0);
-  static const int variant = env_int("MTQ_AMD_QLINEAR_VARIANT", 0);
-  if (variant == 0 && (probe == 0 || M == 1) && (pt || spb == 0)) {
+  if (pt || spb == 0) {
     if (M == 1)
       launch_dma<T, KIND, 1>(g, pt, stream, QL_ARGS);
     else if (M <= 4)
@@ -762,23 +707,7 @@ int launch_stream(const void *x, const void *w, const void *bias, void *y, float
       launch_dma<T, KIND, 8>(g, pt, stream, QL_ARGS);
     else
       launch_dma<T, KIND, 16>(g, pt, stream, QL_ARGS);
-  } else if (pt && probe == 1)
-    qlinear_stream_kernel<T, KIND, kU, true, 0, 1><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (pt && probe == 2)
-    qlinear_stream_kernel<T, KIND, kU, true, 0, 2><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (pt && probe == 3)
-    qlinear_stream_kernel<T, KIND, kU, true, 0, 3><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (pt && probe == 4)
-    qlinear_stream_kernel<T, KIND, kU, true, 0, 4><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (pt && probe == 8)
-    qlinear_stream_kernel<T, KIND, 8, true, 0><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (pt && probe == 9)
-    qlinear_stream_kernel<T, KIND, 8, true, 0, 2><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (pt)
-    qlinear_stream_kernel<T, KIND, kU, true, 0><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (spb == 0)
-    qlinear_stream_kernel<T, KIND, kU, false, 0><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
-  else if (spb == 1)
+  } else if (spb == 1)
     qlinear_stream_kernel<T, KIND, kU, false, 1><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
   else
     qlinear_stream_kernel<T, KIND, kU, false, 2><<<g, kStreamWaves * 64, 0, stream>>>(QL_ARGS);
@@ -804,14 +733,6 @@ int launch_wg(const void *x, const void *w, const void *bias, void *y, int64_t M
   else
     qlinear_wg_kernel<T, KIND, 1, 16, 4><<<g, 16 * 64, 0, stream>>>(xt, wt, bt, yt, M, N, K, p);
   return host_check_launch();
-}
-
-// MTQ_AMD_QLINEAR_VARIANT (A/B measurement): 1 forces the workgroup-per-tile kernel, 2 the
-// register-staged stream kernel; 0 (default) takes the LDS-DMA kernel where the amax layout allows
-bool force_wg() {
-  static int v = -1;
-  if (v < 0) v = env_int("MTQ_AMD_QLINEAR_VARIANT", 0);
-  return v == 1;
 }
 
 bool al16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
@@ -857,7 +778,7 @@ extern "C" int mtq_qlinear_small_m_ws(const void *x, const void *w, const void *
   }
   const int spb = stream_spb(amax_numel, block, K);
   const bool bf = dtype == MTQ_BF16;
-  if (spb < 0 || amax_dtype != 0 || force_wg()) {
+  if (spb < 0 || amax_dtype != 0) {
     if (bf) return kind == 0 ? launch_wg<__bf16, 0>(x, w, bias, y, M, N, K, p, stream)
                              : launch_wg<__bf16, 1>(x, w, bias, y, M, N, K, p, stream);
     return kind == 0 ? launch_wg<_Float16, 0>(x, w, bias, y, M, N, K, p, stream)
@@ -886,11 +807,9 @@ extern "C" int mtq_qlinear_small_m(const void *x, const void *w, const void *bia
 namespace {
 
 // the problems run as one grouped launch: same kind, fp32 amax of one class (per tensor, or
-// per-row blocks aligned to the 128-column batches), the LDS-DMA kernel not switched off
+// per-row blocks aligned to the 128-column batches)
 bool groupable(const mtq_qlinear_problem *pr, int n, int64_t K) {
-  if (n < 1 || n > kMaxGroup || force_wg() || env_int("MTQ_AMD_QLINEAR_VARIANT", 0) != 0 ||
-      env_int("MTQ_AMD_QLINEAR_PROBE", 0) != 0)
-    return false;
+  if (n < 1 || n > kMaxGroup) return false;
   const bool pt = pr[0].amax_numel == 1;
   for (int i = 0; i < n; ++i) {
     if (pr[i].kind != pr[0].kind || pr[i].amax_dtype != 0 || (pr[i].amax_numel == 1) != pt) return false;

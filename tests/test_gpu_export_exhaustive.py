@@ -12,8 +12,7 @@ tests sweep the inputs where that matters:
     divided by non-power-of-two block scales (full-mantissa quotients);
   * FP8 (export/quant_utils.py:855-913): every bf16 / f16 pattern over per-tensor and per-row scales,
     the (448, 464] rounding band and the NaN / overflow bytes.
-The emulated path (MTQ_AMD_EXPORT_NATIVE=0, read once per process) is covered here by the lanes
-that fall back (NaN / overflow quotients, zero divisors, tiny block exponents).
+The emulated path is covered here by the lanes that fall back (NaN / overflow quotients, zero divisors, tiny block exponents).
 """
 
 import pytest
