@@ -2,21 +2,15 @@
 """AWQ-lite alpha search per linear, Llama-3-8B shapes, one calibration batch (8192 tokens, 11
 alphas), all in one process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24):
 
-* ``pp5``     -- mtq_awq_search_gemm mode 2, default schedule 5 (r03 ping-pong kernel + pre-scale
-                 pass; B0 fragments held in registers, every half-tile issued 4-5 phases ahead)
-* ``pp4``     -- schedule 4 (the first r03 schedule, fragments re-read per phase); ``pp4_branch``
-                 the same with the last tile's loads skipped behind a branch (MTQ_AMD_AWQ_PP_CLAMP=0)
-* ``w4``      -- schedule 6: four waves, one per SIMD, 128 x 128 per wave, one barrier per K tile
-* ``*_noload_probe`` -- pp5 / pp4 without global loads in the K loop (skeleton timing; wrong losses)
-* ``r02``     -- mode 1 (r02 kernel, x scaled while register-staged)
-* ``batched`` -- the r02 wide-linear path: awq_prescale + 11 hipBLASLt torch.mm into [G, M, N] +
+* ``fused``   -- mtq_awq_search_gemm: the pre-scale pass + the ping-pong MFMA search kernel with the
+                 loss in its epilogue
+* ``batched`` -- the wide-linear path: awq_prescale + 11 hipBLASLt torch.mm into [G, M, N] +
                  awq_mse_multi
 * ``per_alpha`` -- the r01 path: per alpha mul_cols + hipBLASLt F.linear + mse_accumulate
 * ``hipblaslt_gemms`` -- the 11 bf16 GEMMs alone
 Reports ms (median over rounds) and TFLOP/s = 2*M*N*K*G / time vs the 2.5 PF dense bf16 peak.
 Usage: bench_awq_gemm.py [M] [rounds]"""
 import json
-import os
 import statistics
 import sys
 from pathlib import Path
@@ -46,16 +40,6 @@ def timeit(fn, iters=3):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / iters
-
-
-def with_mode(mode, fn, phases=5, probe=0, clamp=1):
-    def run():
-        os.environ["MTQ_AMD_AWQ_PP_CLAMP"] = str(clamp)
-        os.environ["MTQ_AMD_AWQ_GEMM_MODE"] = str(mode)
-        os.environ["MTQ_AMD_AWQ_PP_PHASES"] = str(phases)
-        os.environ["MTQ_AMD_AWQ_GEMM_PROBE"] = str(probe)
-        fn()
-    return run
 
 
 res = {}
@@ -88,11 +72,7 @@ for name, (N, K) in SHAPES.items():
         for g in range(G):
             F.linear(x, wq[g])
 
-    arms = {"pp5": with_mode(2, search), "pp4": with_mode(2, search, 4),
-            "pp4_branch": with_mode(2, search, 4, clamp=0), "w4": with_mode(2, search, 6),
-            "pp5_noload_probe": with_mode(2, search, 5, 1), "pp4_noload_probe": with_mode(2, search, 4, 1),
-            "r02": with_mode(1, search), "batched": batched,
-            "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
+    arms = {"fused": search, "batched": batched, "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
     t = {k: [] for k in arms}
     for _ in range(ROUNDS):
         for k, f in arms.items():
@@ -103,14 +83,8 @@ for name, (N, K) in SHAPES.items():
         ms = statistics.median(v)
         r[k] = {"ms": round(ms, 3), "min_ms": round(min(v), 3), "tflops": round(flops / (ms * 1e-3) / 1e12, 1)}
         r[k]["frac_of_2.5PF"] = round(r[k]["tflops"] / 2500, 3)
-    r["pp5_speedup_vs_batched"] = round(r["batched"]["ms"] / r["pp5"]["ms"], 3)
-    r["pp5_speedup_vs_per_alpha"] = round(r["per_alpha"]["ms"] / r["pp5"]["ms"], 3)
-    r["pp5_speedup_vs_r02"] = round(r["r02"]["ms"] / r["pp5"]["ms"], 3)
-    r["w4_speedup_vs_pp5"] = round(r["pp5"]["ms"] / r["w4"]["ms"], 3)
+    r["fused_speedup_vs_batched"] = round(r["batched"]["ms"] / r["fused"]["ms"], 3)
+    r["fused_speedup_vs_per_alpha"] = round(r["per_alpha"]["ms"] / r["fused"]["ms"], 3)
     res[name] = r
     print(name, json.dumps(r), file=sys.stderr, flush=True)
-os.environ.pop("MTQ_AMD_AWQ_GEMM_MODE", None)
-os.environ.pop("MTQ_AMD_AWQ_PP_PHASES", None)
-os.environ.pop("MTQ_AMD_AWQ_GEMM_PROBE", None)
-os.environ.pop("MTQ_AMD_AWQ_PP_CLAMP", None)
 print(json.dumps({"M": M, "G": G, "rounds": ROUNDS, "shapes": res}))

@@ -1,0 +1,201 @@
+// hist_exp.hip -- measurement-only variants of the 16-bit pattern histogram (csrc/mtq_kernels.hip
+// hist_value_kernel), built into scripts/exp/libhist_exp.so by scripts/exp/build_exp.sh and timed
+// against the product kernel by scripts/exp/bench_hist_exp.py.  Not part of the product library.
+//
+// VAR bits: 1 = final bin atomics in a per-workgroup rotated order (concurrent workgroups hit
+// different addresses); 2 = two named register batches (A/B) with unconditional, clamped loads --
+// no register copy of an in-flight load and no branch around a load, so the compiler can count
+// vmcnt; 4 = probe: no main loop (zero + fold + flush only); 8 = U * 2 vectors per batch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+constexpr int kThreads = 1024;
+constexpr int kPatterns = 32768;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf16_bits_to_float(uint32_t b) { return __uint_as_float(b << 16); }
+
+template <int U, int VAR>
+__global__ __launch_bounds__(kThreads) void hist_exp_kernel(const uint16_t *__restrict__ x, int64_t nvec,
+                                                            int64_t vec_per_block, const float *hmax, int bins,
+                                                            uint32_t *counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
+  uint32_t *vh = sh;
+  uint32_t *bh = sh + kPatterns;
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  // VAR & 16: only the patterns whose value can be <= hi are zeroed and folded (the largest bf16
+  // pattern p with value(p) <= hi; NaN hi -> nothing counts); the main loop still increments every
+  // pattern, the entries past phi are never read
+  int phi = kPatterns - 1;
+  if constexpr ((VAR & 16) != 0) {
+    if (!(hi >= 0.f)) {
+      phi = -1;
+    } else {
+      uint32_t b = __float_as_uint(hi) >> 16;  // truncation: value(b) <= hi
+      b = b < 0x7F80u ? b : 0x7F80u;
+      phi = (int)b;
+    }
+  }
+  const int nz4 = (phi + 4) / 4;  // uint4 words covering patterns [0, phi]
+  for (int i = threadIdx.x; i < nz4; i += kThreads) reinterpret_cast<uint4 *>(vh)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int b = threadIdx.x; b < bins; b += kThreads) bh[b] = 0;
+  const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
+  int64_t v1 = v0 + vec_per_block;
+  v1 = v1 < nvec ? v1 : nvec;
+  constexpr int64_t kStep = (int64_t)kThreads * U;
+  auto count1 = [&](u32x4 v, bool ok) {
+    const uint32_t w[4] = {ok ? v.x : 0x7FFF7FFFu, ok ? v.y : 0x7FFF7FFFu, ok ? v.z : 0x7FFF7FFFu,
+                           ok ? v.w : 0x7FFF7FFFu};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      atomicAdd(vh + (w[j] & 0x7FFFu), 1u);
+      atomicAdd(vh + ((w[j] >> 16) & 0x7FFFu), 1u);
+    }
+  };
+  int64_t i = v0 + threadIdx.x;
+  if constexpr ((VAR & 4) == 0) {
+    if constexpr (VAR & 2) {
+      const int64_t last = v1 - 1;
+      auto ld = [&](int64_t k) -> u32x4 {
+        const int64_t kc = k < last ? k : last;
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + kc * 8));
+      };
+      u32x4 a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = ld(i + (int64_t)u * kThreads);
+      __syncthreads();
+      for (; i < v1; i += 2 * kStep) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = ld(i + kStep + (int64_t)u * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) count1(a[u], i + (int64_t)u * kThreads < v1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = ld(i + 2 * kStep + (int64_t)u * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) count1(b[u], i + kStep + (int64_t)u * kThreads < v1);
+      }
+    } else {
+      auto load = [&](int64_t ii, u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t k = ii + (int64_t)u * kThreads;
+          if (k < v1)
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + k * 8));
+          else
+            v[u] = u32x4{0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu};
+        }
+      };
+      u32x4 cur[U];
+      load(i, cur);
+      __syncthreads();
+      for (; i < v1; i += kStep) {
+        u32x4 nxt[U];
+        if (i + kStep < v1) load(i + kStep, nxt);
+#pragma unroll
+        for (int u = 0; u < U; ++u) count1(cur[u], true);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+      }
+    }
+  } else {
+    __syncthreads();
+  }
+  __syncthreads();
+  const float fb = (float)bins;
+  const float span = hi - lo;
+  const float y = 1.f / span;
+  const uint32_t lastb = (uint32_t)bins - 1u;
+  auto bin_of = [&](uint32_t p) -> uint32_t {
+    const float a = bf16_bits_to_float(p);
+    const float t = (a - lo) * fb;
+    const float q0 = t * y;
+    const float q = __builtin_fmaf(__builtin_fmaf(-q0, span, t), y, q0);
+    const uint32_t b = (uint32_t)(int)q;
+    return b < lastb ? b : lastb;
+  };
+  if constexpr ((VAR & 32) != 0) {
+    // 4 consecutive patterns per lane (one ds_read_b128; a wave reads 1 KB contiguous), the
+    // counts of equal bins merged in registers before one LDS atomic per run
+    for (int w = threadIdx.x; w < nz4; w += kThreads) {
+      const uint4 c4 = reinterpret_cast<const uint4 *>(vh)[w];
+      const uint32_t cs[4] = {c4.x, c4.y, c4.z, c4.w};
+      uint32_t run_b = 0xFFFFFFFFu, run_c = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t p = (uint32_t)(4 * w + j);
+        if (cs[j] == 0u || (int)p > phi) continue;
+        const float a = bf16_bits_to_float(p);
+        if (!(a <= hi)) continue;
+        const uint32_t b = bin_of(p);
+        if (b != run_b) {
+          if (run_c) atomicAdd(bh + run_b, run_c);
+          run_b = b;
+          run_c = 0;
+        }
+        run_c += cs[j];
+      }
+      if (run_c) atomicAdd(bh + run_b, run_c);
+    }
+  } else {
+    for (int p = threadIdx.x; p <= phi; p += kThreads) {
+      const uint32_t c = vh[p];
+      if (c == 0u) continue;
+      const float a = bf16_bits_to_float((uint32_t)p);
+      if (a <= hi) atomicAdd(bh + bin_of((uint32_t)p), c);
+    }
+  }
+  __syncthreads();
+  const int rot = (VAR & 1) ? (int)((blockIdx.x * 64u) % (unsigned)bins) : 0;
+  for (int bb = threadIdx.x; bb < bins; bb += kThreads) {
+    int b = bb + rot;
+    b = b >= bins ? b - bins : b;
+    if (bh[b]) atomicAdd(counts + b, bh[b]);
+  }
+}
+
+template <int U, int VAR>
+int launch(const void *x, int64_t n, const float *hmax, int bins, uint32_t *counts, hipStream_t stream) {
+  const int64_t nvec = n / 8;
+  int cu = 256;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+  int64_t blocks = cu;
+  const int64_t min_per_block = (int64_t)kThreads * 8;
+  int64_t vpb = (nvec + blocks - 1) / blocks;
+  vpb = vpb < min_per_block ? min_per_block : vpb;
+  blocks = (nvec + vpb - 1) / vpb;
+  const size_t shr = ((size_t)kPatterns + (size_t)bins) * 4;
+  auto kern = hist_exp_kernel<U, VAR>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  kern<<<(unsigned)blocks, kThreads, shr, stream>>>(reinterpret_cast<const uint16_t *>(x), nvec, vpb, hmax, bins,
+                                                    counts);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+}  // namespace
+
+extern "C" int hist_exp(int var, const void *x, int64_t n, const float *hmax, int bins, uint32_t *counts,
+                        hipStream_t stream) {
+  if (n % 8 || bins < 1 || bins > 8192 || ((uintptr_t)x & 15)) return 2;
+  switch (var) {
+  case 0: return launch<2, 0>(x, n, hmax, bins, counts, stream);
+  case 1: return launch<2, 1>(x, n, hmax, bins, counts, stream);
+  case 2: return launch<2, 2>(x, n, hmax, bins, counts, stream);
+  case 3: return launch<2, 3>(x, n, hmax, bins, counts, stream);
+  case 4: return launch<2, 4>(x, n, hmax, bins, counts, stream);
+  case 11: return launch<4, 1>(x, n, hmax, bins, counts, stream);
+  case 13: return launch<4, 3>(x, n, hmax, bins, counts, stream);
+  case 17: return launch<1, 3>(x, n, hmax, bins, counts, stream);
+  case 40: return launch<2, 16>(x, n, hmax, bins, counts, stream);
+  case 41: return launch<2, 48>(x, n, hmax, bins, counts, stream);
+  case 44: return launch<2, 20>(x, n, hmax, bins, counts, stream);
+  case 45: return launch<2, 52>(x, n, hmax, bins, counts, stream);
+  default: return 3;
+  }
+}

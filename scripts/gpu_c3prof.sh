@@ -13,7 +13,7 @@ cat gpurun_out/${TAG}_c3.json
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_trace" -o trace --output-format csv -- python3 "$R/scripts/ptq_llama.py" --config INT4_AWQ_CFG --no-baseline > "$R/gpurun_out/${TAG}_c3_traced.json" 2> "$R/gpurun_out/${TAG}_trace.err" || { tail -20 "$R/gpurun_out/${TAG}_trace.err"; exit 32; }
 cd "$R"
-python3 scripts/trace_gaps.py gpurun_out/${TAG}_trace/*/trace_kernel_trace.csv gpurun_out/${TAG}_gaps.json > /dev/null || true
+python3 scripts/trace_gaps.py gpurun_out/${TAG}_trace/trace_kernel_trace.csv gpurun_out/${TAG}_gaps.json > /dev/null || true
 find gpurun_out/${TAG}_trace -type f ! -name "*stats.csv" -delete
 head -30 gpurun_out/${TAG}_trace/*/trace_kernel_stats.csv 2>/dev/null | cut -c1-200 || true
 echo ok

@@ -45,31 +45,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <typename T> struct Mfma32;
-template <> struct Mfma32<__bf16> {
-  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
-  static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct Mfma32<_Float16> {
-  typedef _Float16 v8 __attribute__((ext_vector_type(8)));
-  static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-  }
-};
-
-// LDS-DMA (global_load_lds) data is visible to other waves only after the issuing wave's vmcnt
-// drain and a barrier (cdna_hip_programming.md §5 'Read a staged buffer one phase AFTER ...')
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 constexpr int kBM = 256, kBN = 256, kBK = 64, kThreads = 512;
-constexpr int kTileBytes = kBM * kBK * 2;  // 32 KiB per operand tile (bf16/f16)
-constexpr int kLdsBytes = 4 * kTileBytes;  // A[2] + B[2]
-
-// byte offset of 16-byte chunk c (0..7) of row r in a [rows][64] 16-bit tile
-__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
-
 struct AwqGemmArgs {
   const void *x;     // [M, K]
   const void *sinv;  // [G, K]
@@ -80,244 +56,6 @@ struct AwqGemmArgs {
   int64_t M, N, K;
   int tiles_m, tiles_n, G;
 };
-
-// PROBE (measurement builds only, MTQ_AMD_AWQ_GEMM_PROBE): 1 = no global loads / LDS staging in
-// the K loop (the ds_read + MFMA + barrier structure alone), 2 = no epilogue loads.
-// PRE: x holds the pre-scaled activations xs [G, M, K] (mtq_awq_prescale_kernel) and both tiles
-// come in by LDS-DMA; otherwise x [M, K] is scaled while being register-staged.
-template <typename T, bool PRE, int PROBE = 0>
-__global__ __launch_bounds__(kThreads) void awq_search_gemm_kernel(AwqGemmArgs p) {
-  typedef typename Mfma32<T>::v8 v8;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[kLdsBytes];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-
-  // XCD-aware remap (bijective for any grid size): blocks that share an XCD get consecutive ids
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int tiles = p.tiles_m * p.tiles_n;
-  const int g = wgid / tiles;
-  const int tile = wgid - g * tiles;
-  // grouped order: the ~32 workgroups an XCD runs at once cover 8 row tiles x 4 column tiles,
-  // so each K slice of their A and W tiles comes from beyond L2 once per group (12 slices per
-  // 32 tiles instead of 33 with a plain row-major walk)
-  constexpr int kGroupM = 8;
-  const int grp = tile / (kGroupM * p.tiles_n);
-  const int first_m = grp * kGroupM;
-  const int gsz = p.tiles_m - first_m < kGroupM ? p.tiles_m - first_m : kGroupM;
-  const int tin = tile - grp * kGroupM * p.tiles_n;
-  const int tm = first_m + tin % gsz, tn = tin / gsz;
-  const int64_t m0 = (int64_t)tm * kBM, n0 = (int64_t)tn * kBN;
-  const int64_t K = p.K;
-
-  const T *X = reinterpret_cast<const T *>(p.x) + (PRE ? (int64_t)g * p.M * K : 0);
-  const T *S = reinterpret_cast<const T *>(p.sinv) + (int64_t)g * K;
-  const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
-
-  // ---- A (x) staging: thread owns chunk c = tid & 7 of rows (tid >> 3) + 64 u, u = 0..3
-  // (32-bit element offsets from wave-uniform bases: the launcher checks M*K, N*K < 2^31)
-  const int a_c = tid & 7, a_r0 = tid >> 3;
-  unsigned a_off[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int r = a_r0 + 64 * u;
-    int64_t row = m0 + r;
-    row = row < p.M ? row : p.M - 1;  // clamp: rows past M are computed and masked
-    // register staging writes the swizzled position itself; the DMA needs it on the source
-    a_off[u] = (unsigned)(row * K + (PRE ? ((a_c ^ ((r >> 1) & 7)) * 8) : a_c * 8));
-  }
-  // ---- B (wq) staging by global_load_lds: round u writes LDS bytes [u * 8 KiB + tid * 16)
-  const int b_row0 = tid >> 3, b_cs = tid & 7;  // LDS row u*64 + b_row0, chunk slot b_cs
-  unsigned b_off[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int r = u * 64 + b_row0;
-    int64_t row = n0 + r;
-    row = row < p.N ? row : p.N - 1;
-    b_off[u] = (unsigned)(row * K + ((b_cs ^ ((r >> 1) & 7)) * 8));
-  }
-
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-  u32x4_t areg[4];
-  u32x4_t sreg;
-  auto load_a = [&](int64_t k0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) areg[u] = *reinterpret_cast<const u32x4_t *>(X + k0 + a_off[u]);
-    sreg = *reinterpret_cast<const u32x4_t *>(S + k0 + a_c * 8);
-  };
-  auto store_a = [&](unsigned char *abuf) {
-    // opaque barrier: keeps the unpacking of the prefetched registers after the MFMAs (hipcc
-    // otherwise hoists it next to the loads and waits vmcnt(0) before the tile's compute)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) asm volatile("" : "+v"(areg[u]));
-    asm volatile("" : "+v"(sreg));
-    Vec<T> s;
-    __builtin_memcpy(&s.raw, &sreg, 16);
-    float sf[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sf[j] = Elem<T>::ld(s.e[j]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      Vec<T> v;
-      __builtin_memcpy(&v.raw, &areg[u], 16);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v.e[j] = Elem<T>::st(Elem<T>::ld(v.e[j]) * sf[j]);  // T(x * (1/s))
-      *reinterpret_cast<uint4 *>(abuf + swz(a_r0 + 64 * u, a_c)) = v.raw;
-    }
-  };
-  auto load_a_dma = [&](unsigned char *abuf, int64_t k0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void *)(X + k0 + a_off[u]),
-          (__attribute__((address_space(3))) void *)(abuf + u * 8192 + wave * 1024), 16, 0, 0);
-  };
-  auto load_b = [&](unsigned char *bbuf, int64_t k0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void *)(W + k0 + b_off[u]),
-          (__attribute__((address_space(3))) void *)(bbuf + u * 8192 + wave * 1024), 16, 0, 0);
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  unsigned char *const A0 = lds, *const B0 = lds + 2 * kTileBytes;
-  const int nt = (int)(K / kBK);
-  const int fr = lane & 31, fh = lane >> 5;
-  auto kclamp = [&](int t) { return (int64_t)(t < nt ? t : nt - 1) * kBK; };
-  auto read_frags = [&](const unsigned char *Ac, const unsigned char *Bc, int s, v8 *a, v8 *b) {
-    const int ch = 2 * s + fh;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v8 *>(Ac + swz(wm * 128 + i * 32 + fr, ch));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const v8 *>(Bc + swz(wn * 64 + j * 32 + fr, ch));
-  };
-  auto mfma8 = [&](const v8 *a, const v8 *b) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = Mfma32<T>::mma(a[i], b[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // Pipeline (per K step t, buffers cur = t & 1):
-  //   the x registers hold tile t+1 (loaded during step t-1) -> scaled into A[cur^1] early in
-  //   step t, then re-filled with tile t+2; W tile t+1 goes to B[cur^1] by LDS-DMA at the top of
-  //   step t.  The step ends with a counted vmcnt that retires only the DMA (the 5 x loads issued
-  //   after it stay in flight across the raw barrier) -> every load has a full step to land.
-  if (PRE) {
-    load_a_dma(A0, 0);
-    load_b(B0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    load_a(0);
-    load_b(B0, 0);
-    store_a(A0);  // waits for the x registers (and, in order, nothing after them)
-    load_a(kclamp(1));
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // W tile 0 landed; x tile 1 in flight
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    const unsigned char *Ac = A0 + cur * kTileBytes, *Bc = B0 + cur * kTileBytes;
-    if (PRE && PROBE != 1) {
-      // both tiles of step t+1 by LDS-DMA into the idle buffers (last read in step t-1, before
-      // the barrier that ended it): a whole step of MFMAs to land
-      load_a_dma(A0 + (cur ^ 1) * kTileBytes, kclamp(t + 1));
-      load_b(B0 + (cur ^ 1) * kTileBytes, kclamp(t + 1));
-    }
-    v8 a0[4], b0[2], a1[4], b1[2];
-    read_frags(Ac, Bc, 0, a0, b0);
-    read_frags(Ac, Bc, 1, a1, b1);
-    mfma8(a0, b0);
-    if (!PRE && PROBE != 1) {
-      // x tile t+1 -> LDS, its VALU beside the MFMAs.  hipcc waits vmcnt(0) before the first
-      // use of the x registers, so the W DMA of tile t+1 is issued after it, not before.
-      store_a(A0 + (cur ^ 1) * kTileBytes);
-      // keep the ds_writes ahead of the DMA: a ds_write behind an LDS-DMA in flight makes
-      // hipcc drain vmcnt(0) first (it cannot tell the two LDS ranges apart)
-      __builtin_amdgcn_sched_barrier(0);
-      load_b(B0 + (cur ^ 1) * kTileBytes, kclamp(t + 1));
-      load_a(kclamp(t + 2));
-    }
-    read_frags(Ac, Bc, 2, a0, b0);
-    mfma8(a1, b1);
-    read_frags(Ac, Bc, 3, a1, b1);
-    mfma8(a0, b0);
-    mfma8(a1, b1);
-    if (PRE)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // this step's W DMA retired
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // ---- epilogue: bias, round to T, difference vs yref rounded to T, fp32 square-sum.
-  // The yref tile [256 x 256] is staged through LDS (all 16 DMA rounds in flight at once, one
-  // memory latency) and read back in the accumulator layout; rows past M / chunks past N are
-  // clamped on load and masked below (N % 8 == 0).
-  const T *Y = reinterpret_cast<const T *>(p.yref);
-  const T *Bi = reinterpret_cast<const T *>(p.bias);
-  if (PROBE != 2) {
-    const int rl = wave * 2 + (lane >> 5), ck = lane & 31;
-    int64_t col = n0 + ck * 8;
-    col = col < p.N ? col : p.N - 8;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      int64_t row = m0 + u * 16 + rl;
-      row = row < p.M ? row : p.M - 1;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
-          (__attribute__((address_space(3))) void *)(lds + u * 8192 + wave * 1024), 16, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float sum = 0.f;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int cl = wn * 64 + j * 32 + fr;  // column within the tile
-    const bool cok = n0 + cl < p.N;
-    const float bj = Bi ? Elem<T>::ld(Bi[cok ? n0 + cl : p.N - 1]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rl = wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
-        const T yr = *reinterpret_cast<const T *>(lds + rl * 512 + cl * 2);
-        const float y = Elem<T>::ld(Elem<T>::st(acc[i][j][e] + bj));
-        const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr)));
-        sum = (cok && m0 + rl < p.M) ? __builtin_fmaf(d, d, sum) : sum;
-      }
-    }
-  }
-  __syncthreads();  // the LDS tile is reused for the reduction below
-  // fixed-order reduction: wave butterfly, then the 8 waves in order
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
-  float *red = reinterpret_cast<float *>(lds);
-  if (lane == 0) red[wave] = sum;
-  __syncthreads();
-  if (tid == 0) {
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; ++w) s += red[w];
-    p.partial[(int64_t)g * tiles + tile] = s;
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // r03 search kernel: two wave groups in ping-pong, half-tile LDS-DMA ring, counted vmcnt.
@@ -368,13 +106,29 @@ template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// PROBE (measurement builds only, MTQ_AMD_AWQ_GEMM_PROBE=1): no global loads in the K loop -- the
-// ds_read + MFMA + barrier skeleton alone (the loss is then meaningless)
-// CLAMP (PH 4): the last K tile re-loads itself (no branch in the loop) instead of skipping its
-// loads (PH 5 always clamps).  Variants measured and dropped in r03 (profiles/r03/awq): two phases
-// per K tile, the untransposed MFMA orientation, reference rows by direct loads, DMA rounds
-// interleaved into the MFMA burst -- none faster than PH 5.
-template <typename T, bool HAS_BIAS, int PH, int PROBE = 0, bool CLAMP = true>
+// buffer descriptor from wave-uniform inputs (cdna_hip_programming.md T20: no waterfall loops)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
+
+// buffer_load_dwordx4 ... lds (16 B per lane).  The builtin exists only in the device pass; named
+// in a kernel body seen by the host pass it drops that kernel's host stub, hence the guard.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define AWQ_DMA(rsrc, lds, voff, soff) \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds((rsrc), (__attribute__((address_space(3))) void *)(lds), 16, (voff), (soff), 0, 0)
+#else
+#define AWQ_DMA(rsrc, lds, voff, soff) ((void)(rsrc), (void)(lds), (void)(voff), (void)(soff))
+#endif
+
+// Variants measured and dropped (profiles/r03/awq, profiles/r04/awq): two phases per K tile, the
+// untransposed MFMA orientation, reference rows by direct loads, DMA rounds interleaved into the
+// MFMA burst, fragments re-read per phase (r03 schedule 4), one 128 x 128 wave per SIMD (W4),
+// 4 or 16 row tiles per XCD group, buffer_load ... lds instead of global_load_lds.
+template <typename T, bool HAS_BIAS>
 __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) {
   using namespace pp;
   typedef typename Mfma16<T>::v8 v8;
@@ -383,19 +137,30 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wn = wave & 3;
 
-  // XCD-aware remap + grouped tile order, as the r02 kernel
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q8 = nwg / 8, rr8 = nwg % 8, xcd = orig % 8;
-  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + orig / 8;
+  // Tile order (r04): units of 8 row tiles x 4 column tiles, one per XCD round (32 workgroups =
+  // the XCD's 32 CUs; the 8 x 4 shape maximises the K-slice reuse in the XCD's L2: 12 slices per
+  // K step for 32 tiles).  Unit u = ((g * NN4) + n4) * MGN + mg runs on XCD u % 8 in local round
+  // u / 8 (blocks are dispatched to XCDs round-robin by blockIdx % 8 -- a speed assumption only,
+  // any placement is correct), so the eight XCDs work on the SAME alpha and column range at once,
+  // on different row groups: every W panel comes from HBM once and is shared through the
+  // Infinity Cache, and the alpha's activations stay resident there (r03 gave each XCD a
+  // contiguous range of the whole grid, so each W panel was fetched once per row group).
+  // Measured (scripts/exp/awq_exp.hip, profiles/r04/awq): gate_proj 7.89 -> 7.77 ms, q_proj 2.30
+  // -> 2.20 ms; with the buffer-DMA below 7.70 / 2.17.  Slots past the matrix edge exit at once.
+  const int orig = blockIdx.x;
   const int tiles = p.tiles_m * p.tiles_n;
-  const int g = wgid / tiles;
-  const int tile = wgid - g * tiles;
-  constexpr int kGroupM = 8;
-  const int gm = tile / (kGroupM * p.tiles_n);
-  const int first_m = gm * kGroupM;
-  const int gsz = p.tiles_m - first_m < kGroupM ? p.tiles_m - first_m : kGroupM;
-  const int tin = tile - gm * kGroupM * p.tiles_n;
-  const int tm = first_m + tin % gsz, tn = tin / gsz;
+  int g, tm, tn;
+  {
+    const int xcd = orig % 8, li = orig / 8;
+    const int slot = li % 32, u = (li / 32) * 8 + xcd;
+    const int mgn = (p.tiles_m + 7) / 8, nn4 = (p.tiles_n + 3) / 4;
+    const int mg = u % mgn, n4 = (u / mgn) % nn4;
+    g = u / (mgn * nn4);
+    tm = mg * 8 + slot % 8;
+    tn = n4 * 4 + slot / 8;
+    if (g >= p.G || tm >= p.tiles_m || tn >= p.tiles_n) return;  // the whole workgroup, before any barrier
+  }
+  const int tile = tm * p.tiles_n + tn;
   const int64_t m0 = (int64_t)tm * kBM, n0 = (int64_t)tn * kBN;
   const int64_t K = p.K;
   const T *X = reinterpret_cast<const T *>(p.x) + (int64_t)g * p.M * K;
@@ -417,22 +182,19 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
       col = col < p.N ? col : p.N - 1;
       b_off[h][u] = (unsigned)(col * K + chunk * 8);
     }
-  auto dma = [&](const T *base, unsigned off, unsigned char *dst) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(base + off),
-                                     (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
-  };
+  // buffer_load ... lds through one descriptor per operand: the per-lane offset is loop-invariant
+  // and the K advance is the scalar offset (global_load_lds needed a 64-bit address per DMA;
+  // 1-2 % faster, scripts/exp/awq_exp.hip)
+  const __amdgpu_buffer_rsrc_t xr = wave_rsrc(X, (uint32_t)(p.M * K * 2));
+  const __amdgpu_buffer_rsrc_t wr = wave_rsrc(W, (uint32_t)(p.N * K * 2));
   // half index q of K tile at k0 into buffer buf: q = 0 A0, 1 B0, 2 B1, 3 A1
   auto load_half = [&](int q, unsigned char *buf, int64_t k0) {
     const bool isA = (q == 0 || q == 3);
     const int h = (q == 0 || q == 1) ? 0 : 1;
     unsigned char *dst = buf + (isA ? h : 2 + h) * kHalf + wave * 1024;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(k0 * 2));
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (isA)
-        dma(X + k0, a_off[h][u], dst + u * 8192);
-      else
-        dma(W + k0, b_off[h][u], dst + u * 8192);
-    }
+    for (int u = 0; u < 2; ++u) AWQ_DMA(isA ? xr : wr, dst + u * 8192, (isA ? a_off[h][u] : b_off[h][u]) * 2u, soff);
   };
 
   // ---- fragment reads: A m-tile i (16 rows) / B n-tile j, k-step s (32 of the tile's 64)
@@ -453,9 +215,9 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (int)(K / kBK);
-  // prologue: K tile 0 in full (A0 B0 B1 A1); phase 0 needs A0 and B0
-  if constexpr (PH == 5) {
-    // stream order B0 A0 B1 A1 of tile 0, then B0 A0 of tile 1 (see the PH 5 loop)
+  // prologue: K tile 0 in full in the stream order B0 A0 B1 A1, then B0 A0 of tile 1 (the loop's
+  // phases 2 and 3 of a virtual tile -1); phase 0 needs A0 and B0
+  {
     const int64_t k1 = (int64_t)(nt > 1 ? 1 : 0) * kBK;
     load_half(1, lds, 0);
     load_half(0, lds, 0);
@@ -464,119 +226,67 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
     load_half(1, lds + kBuf, k1);
     load_half(0, lds + kBuf, k1);
     wait_vm<8>();
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) load_half(q, lds, 0);
-    wait_vm<4>();
   }
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger (wave-uniform: scalar branch)
 
-  if constexpr (PH == 5) {
-    // Four phases per K tile as PH 4, but the B0 fragments (n-quadrant 0, used by the first and
-    // the last phase) stay in registers from phase 0 to phase 3, so every half-tile's last LDS
-    // read is early: A0 phase 1, B0 phase 0, B1 phase 2, A1 phase 3 (phase 3 reads nothing).
-    // Each half of tile t+2 / t+1 can then be loaded two phases after the same half of tile t /
-    // t-1 was last read (the stagger margin) and still has 4-5 phases to land:
-    //   phase 0: B1(t+1) -> buffer t+1     phase 2: B0(t+2) -> buffer t (B0(t) is in registers)
-    //   phase 1: A1(t+1) -> buffer t+1     phase 3: A0(t+2) -> buffer t (A0(t) read in phase 1)
-    // Waits (before each phase's first barrier, for the next phase's reads): vmcnt(8) -- four
-    // halves issued after the one needed may stay in flight -- and vmcnt(10) in phase 2, whose
-    // successor reads nothing new.
-    v8 af[4][2], b0f[2][2], b1f[2][2];
-    for (int t = 0; t < nt; ++t) {
-      unsigned char *cur = lds + (t & 1) * kBuf;
-      unsigned char *nx1 = lds + ((t + 1) & 1) * kBuf;
-      const int64_t k1 = (int64_t)(t + 1 < nt ? t + 1 : nt - 1) * kBK;  // past the end: harmless re-loads
-      const int64_t k2 = (int64_t)(t + 2 < nt ? t + 2 : nt - 1) * kBK;
+  // Four phases per K tile.  The B0 fragments (n-quadrant 0, used by the first and the last
+  // phase) stay in registers from phase 0 to phase 3, so every half-tile's last LDS
+  // read is early: A0 phase 1, B0 phase 0, B1 phase 2, A1 phase 3 (phase 3 reads nothing).
+  // Each half of tile t+2 / t+1 can then be loaded two phases after the same half of tile t /
+  // t-1 was last read (the stagger margin) and still has 4-5 phases to land:
+  //   phase 0: B1(t+1) -> buffer t+1     phase 2: B0(t+2) -> buffer t (B0(t) is in registers)
+  //   phase 1: A1(t+1) -> buffer t+1     phase 3: A0(t+2) -> buffer t (A0(t) read in phase 1)
+  // Waits (before each phase's first barrier, for the next phase's reads): vmcnt(8) -- four
+  // halves issued after the one needed may stay in flight -- and vmcnt(10) in phase 2, whose
+  // successor reads nothing new.
+  v8 af[4][2], b0f[2][2], b1f[2][2];
+  for (int t = 0; t < nt; ++t) {
+    unsigned char *cur = lds + (t & 1) * kBuf;
+    unsigned char *nx1 = lds + ((t + 1) & 1) * kBuf;
+    const int64_t k1 = (int64_t)(t + 1 < nt ? t + 1 : nt - 1) * kBK;  // past the end: harmless re-loads
+    const int64_t k2 = (int64_t)(t + 2 < nt ? t + 2 : nt - 1) * kBK;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int mq = (q == 0 || q == 1) ? 0 : 1;
-        const int nq = (q == 1 || q == 2) ? 1 : 0;
-        if (q == 0 || q == 2) {
+    for (int q = 0; q < 4; ++q) {
+      const int mq = (q == 0 || q == 1) ? 0 : 1;
+      const int nq = (q == 1 || q == 2) ? 1 : 0;
+      if (q == 0 || q == 2) {
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i][s2] = read_a(cur, 4 * mq + i, s2);
-        }
-        if (q == 0) {
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) b0f[j][s2] = read_b(cur, j, s2);
-        }
-        if (q == 1) {
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) b1f[j][s2] = read_b(cur, 2 + j, s2);
-        }
-        // this phase's half: q0 B1(t+1), q1 A1(t+1) -> buffer t+1; q2 B0(t+2), q3 A0(t+2) -> buffer t
-        const int hq = q == 0 ? 2 : q == 1 ? 3 : q == 2 ? 1 : 0;
-        unsigned char *hb = q < 2 ? nx1 : cur;
-        const int64_t hk = q < 2 ? k1 : k2;
-        if (PROBE == 0) {
-          load_half(hq, hb, hk);
-          if (q == 2)
-            wait_vm<10>();
-          else
-            wait_vm<8>();
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-          const int s2 = kk >> 3, j = (kk >> 2) & 1, i = kk & 3;
-          const v8 bb = nq ? b1f[j][s2] : b0f[j][s2];
-          acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bb, af[i][s2], acc[4 * mq + i][2 * nq + j]);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
+          for (int i = 0; i < 4; ++i) af[i][s2] = read_a(cur, 4 * mq + i, s2);
       }
-    }
-  } else {
-    static_assert(PH == 4, "PH 4 or 5");
-    v8 af[4][2], bf[2][2];
-    for (int t = 0; t < nt; ++t) {
-      unsigned char *cur = lds + (t & 1) * kBuf;
-      unsigned char *nxt = lds + ((t + 1) & 1) * kBuf;
-      const int64_t kn = (int64_t)(CLAMP ? (t + 1 < nt ? t + 1 : nt - 1) : t + 1) * kBK;
-      const bool more = PROBE == 0 && (CLAMP || t + 1 < nt);  // the last tile loads nothing and drains
+      if (q == 0) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int mq = (q == 0 || q == 1) ? 0 : 1;
-        const int nq = (q == 1 || q == 2) ? 1 : 0;
-        if (q == 0 || q == 2) {
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) af[i][s] = read_a(cur, 4 * mq + i, s);
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) bf[j][s] = read_b(cur, 2 * nq + j, s);
-        if (more) {
-          load_half(q, nxt, kn);
-          if (q == 2)
-            wait_vm<6>();
-          else
-            wait_vm<4>();
-        } else {
-          wait_vm<0>();
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)  // the A operand (W fragment) held for 4 MFMAs
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bf[j][s], af[i][s], acc[4 * mq + i][2 * nq + j]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
+          for (int j = 0; j < 2; ++j) b0f[j][s2] = read_b(cur, j, s2);
       }
+      if (q == 1) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) b1f[j][s2] = read_b(cur, 2 + j, s2);
+      }
+      // this phase's half: q0 B1(t+1), q1 A1(t+1) -> buffer t+1; q2 B0(t+2), q3 A0(t+2) -> buffer t
+      const int hq = q == 0 ? 2 : q == 1 ? 3 : q == 2 ? 1 : 0;
+      unsigned char *hb = q < 2 ? nx1 : cur;
+      const int64_t hk = q < 2 ? k1 : k2;
+      load_half(hq, hb, hk);
+      if (q == 2)
+        wait_vm<10>();
+      else
+        wait_vm<8>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int s2 = kk >> 3, j = (kk >> 2) & 1, i = kk & 3;
+        const v8 bb = nq ? b1f[j][s2] : b0f[j][s2];
+        acc[4 * mq + i][2 * nq + j] = Mfma16<T>::mma(bb, af[i][s2], acc[4 * mq + i][2 * nq + j]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
     }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
@@ -665,221 +375,59 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// W4 (mode 2, MTQ_AMD_AWQ_PP_PHASES=6): four waves, ONE wave per SIMD, each wave a 128 x 128 block
-// of the 256 x 256 tile (8 x 8 tiles of 16x16x32, 256 accumulator registers: VGPR + AGPR file of a
-// 512-register wave).  Per K tile (64) a wave reads 32 KiB of fragments (2/3 of the two-group
-// layout's LDS traffic per MFMA) and meets ONE barrier:
-//   phase A: MFMAs of k-step 0 (64) with the k-step 1 fragments of the same tile read beside them;
-//   vmcnt(0) (tile t+1 landed) + lgkmcnt(0), barrier;
-//   phase B: MFMAs of k-step 1 (64) with the k-step 0 fragments of tile t+1 read and tile t+2's
-//            16 LDS-DMA rounds issued into the buffer tile t just vacated.
-// Tile t+2's loads then have phase B of tile t and phase A of tile t+1 (~2k MFMA cycles) to land.
-// Fragments are double-buffered in registers (F0 / F1).  Epilogue as the pp kernel (transposed
-// accumulators, reference rows by 8-byte loads).
-// the accumulators pinned to AGPRs ("+a"): hipcc otherwise shuffles the 256 loop-carried
-// accumulators between the two register files every iteration (v_accvgpr_read/write/mov)
-template <typename T>
-__device__ __forceinline__ void mma_agpr(f32x4 &c, typename Mfma16<T>::v8 a, typename Mfma16<T>::v8 b) {
-  if constexpr (__is_same(T, __bf16))
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-  else
-    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-
-template <typename T, bool HAS_BIAS>
-__global__ __launch_bounds__(256, 1) void awq_search_w4_kernel(AwqGemmArgs p) {
-  typedef typename Mfma16<T>::v8 v8;
-  constexpr int kStage = 65536;  // A [256][64] + B [256][64] bf16/f16
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kStage];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q8 = nwg / 8, rr8 = nwg % 8, xcd = orig % 8;
-  const int wgid = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + orig / 8;
-  const int tiles = p.tiles_m * p.tiles_n;
-  const int g = wgid / tiles;
-  const int tile = wgid - g * tiles;
-  constexpr int kGroupM = 8;
-  const int gm = tile / (kGroupM * p.tiles_n);
-  const int first_m = gm * kGroupM;
-  const int gsz = p.tiles_m - first_m < kGroupM ? p.tiles_m - first_m : kGroupM;
-  const int tin = tile - gm * kGroupM * p.tiles_n;
-  const int tm = first_m + tin % gsz, tn = tin / gsz;
-  const int64_t m0 = (int64_t)tm * kBM, n0 = (int64_t)tn * kBN;
-  const int64_t K = p.K;
-  const T *X = reinterpret_cast<const T *>(p.x) + (int64_t)g * p.M * K;
-  const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
-
-  // LDS-DMA: round u (0..7) of an operand writes image bytes [u * 4 KiB + tid * 16): row
-  // u * 32 + (tid >> 3), chunk slot tid & 7 holding source chunk slot ^ ((row >> 1) & 7)
-  unsigned a_off[8], b_off[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int row = u * 32 + (tid >> 3);
-    const int chunk = (tid & 7) ^ ((row >> 1) & 7);
-    int64_t ra = m0 + row;
-    ra = ra < p.M ? ra : p.M - 1;
-    a_off[u] = (unsigned)(ra * K + chunk * 8);
-    int64_t rb = n0 + row;
-    rb = rb < p.N ? rb : p.N - 1;
-    b_off[u] = (unsigned)(rb * K + chunk * 8);
-  }
-  auto dma = [&](const T *base, unsigned off, unsigned char *dst) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(base + off),
-                                     (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
-  };
-  auto load_a = [&](unsigned char *stage, int64_t k0, int u) { dma(X + k0, a_off[u], stage + u * 4096 + wave * 1024); };
-  auto load_b = [&](unsigned char *stage, int64_t k0, int u) {
-    dma(W + k0, b_off[u], stage + 32768 + u * 4096 + wave * 1024);
-  };
-  const int sw = (lane >> 1) & 7, fr = lane & 15, fq = lane >> 4;
-  auto read_a = [&](const unsigned char *stage, int i, int s) -> v8 {
-    const int L = wm * 128 + 16 * i + fr;
-    return *reinterpret_cast<const v8 *>(stage + L * 128 + (((4 * s + fq) ^ sw) << 4));
-  };
-  auto read_b = [&](const unsigned char *stage, int j, int s) -> v8 {
-    const int L = wn * 128 + 16 * j + fr;
-    return *reinterpret_cast<const v8 *>(stage + 32768 + L * 128 + (((4 * s + fq) ^ sw) << 4));
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nt = (int)(K / kBK);
-  auto kof = [&](int t) -> int64_t { return (int64_t)(t < nt ? t : nt - 1) * kBK; };
-  // prologue: tiles 0 and 1 (a clamped re-load of tile 0 when K = 64), tile 0's k-step 0 fragments
-#pragma unroll
-  for (int u = 0; u < 8; ++u) { load_a(lds, 0, u); load_b(lds, 0, u); }
-#pragma unroll
-  for (int u = 0; u < 8; ++u) { load_a(lds + kStage, kof(1), u); load_b(lds + kStage, kof(1), u); }
-  wait_vm<16>();
-  __syncthreads();
-  // registers: A fragments double-buffered (fa0 / fa1, 64 VGPRs), B fragments rotating in place
-  // (fb[j] is re-read for the next k-step as soon as its 8 MFMAs are issued, 32 VGPRs)
-  v8 fa0[8], fa1[8], fb[8];
-  // the asm MFMAs are opaque to hipcc's hazard padding (cdna_hip_programming.md §5.7 item 2):
-  // wait states between the compiler's accumulator initialisation and the first MFMA here, and
-  // between the last MFMA and the compiler's accumulator reads after the loop
-  asm volatile("s_nop 4" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) fa0[i] = read_a(lds, i, 0);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) fb[j] = read_b(lds, j, 0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // loop entry with no LDS read pending (as the back-edge)
-
-  for (int t = 0; t < nt; ++t) {
-    unsigned char *cur = lds + (t & 1) * kStage;
-    unsigned char *nxt = lds + ((t + 1) & 1) * kStage;
-    // ---- phase A: k-step 0 of tile t; the k-step 1 fragments of tile t read beside it
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa1[i] = read_a(cur, i, 1);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) mma_agpr<T>(acc[i][j], fb[j], fa0[i]);
-      fb[j] = read_b(cur, j, 1);
-    }
-    wait_vm<0>();  // tile t+1 (this wave's rounds) landed
-    // lgkmcnt(0) through the builtin, which hipcc's wait insertion sees (an asm one it does not,
-    // and it would then wait lgkmcnt(0) again before the first MFMA of the next phase)
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase B: k-step 1 of tile t; tile t+1's k-step 0 fragments and tile t+2's DMA
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa0[i] = read_a(nxt, i, 0);
-    const int64_t k2 = kof(t + 2);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      // two of tile t+2's sixteen DMA rounds per 8 MFMAs, spread over the phase (issuing all sixteen
-      // up front stalls the wave's MFMA issue behind them: 9.9 vs 8.8 ms on gate_proj,
-      // profiles/r03/awq/search_bench_w4_front.json)
-      load_a(cur, k2, j);
-      load_b(cur, k2, j);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) mma_agpr<T>(acc[i][j], fb[j], fa1[i]);
-      fb[j] = read_b(nxt, j, 0);
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // the next phase A then starts without a wait
-  }
-  wait_vm<0>();
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-
-  // ---- epilogue: lane holds out[m][n .. n+3], m = wm*128 + 16 i + fr, n = wn*128 + 16 j + 4 fq
-  const T *Y = reinterpret_cast<const T *>(p.yref);
-  const T *Bi = reinterpret_cast<const T *>(p.bias);
-  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-  float sum = 0.f;
-#pragma unroll
-  for (int jh = 0; jh < 2; ++jh) {  // two halves of the columns: 32 reference loads in flight each
-    u32x2_t yv[8][4];
-    bool cok[4];
-    int64_t coln[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int64_t c = n0 + wn * 128 + 16 * (4 * jh + jj) + 4 * fq;
-      cok[jj] = c < p.N;
-      coln[jj] = cok[jj] ? c : p.N - 4;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int64_t r = m0 + wm * 128 + 16 * i + fr;
-      r = r < p.M ? r : p.M - 1;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) yv[i][jj] = *reinterpret_cast<const u32x2_t *>(Y + r * p.N + coln[jj]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const bool rok = m0 + wm * 128 + 16 * i + fr < p.M;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        T yr[4];
-        __builtin_memcpy(yr, &yv[i][jj], 8);
-        const bool ok = rok && cok[jj];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float bj = HAS_BIAS ? Elem<T>::ld(Bi[coln[jj] + e]) : 0.f;
-          const float y = Elem<T>::ld(Elem<T>::st(acc[i][4 * jh + jj][e] + bj));
-          const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yr[e])));
-          sum = ok ? __builtin_fmaf(d, d, sum) : sum;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
-  __syncthreads();
-  float *red = reinterpret_cast<float *>(lds);
-  if (lane == 0) red[wave] = sum;
-  __syncthreads();
-  if (tid == 0) p.partial[(int64_t)g * tiles + tile] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
 // xs[g, m, k] = T(x[m, k] * sinv[g, k]) for all g: one read of x, G writes (the reference's
-// `inputs * pre_quant_scale` per alpha, tensor_quantizer.py:1143-1144)
-template <typename T>
+// `inputs * pre_quant_scale` per alpha, tensor_quantizer.py:1143-1144).  GT > 0: the alpha count
+// as a compile-time constant, so every sinv load of the thread is issued before the first product
+// (the runtime-G loop waited for each L2 round trip in turn: 197 us = 4.1 TB/s at [8192, 4096] x
+// 11 in the r04 C3 profile); the G output planes stream out with non-temporal stores (written
+// once, read once by the next GEMM, 11x larger than the Infinity Cache).
+template <typename T, int GT>
 __global__ __launch_bounds__(256) void awq_prescale_kernel(const T *__restrict__ x, const T *__restrict__ sinv,
                                                            T *__restrict__ xs, int64_t chunks, int64_t kchunks,
                                                            int G) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= chunks) return;
-  Vec<T> v = ldg_vec(x + c * 8);
-  float xf[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) xf[j] = Elem<T>::ld(v.e[j]);
   const int64_t kc = c % kchunks;
-  for (int g = 0; g < G; ++g) {
-    Vec<T> s = ldg_vec(sinv + ((int64_t)g * kchunks + kc) * 8);
-    Vec<T> o;
+  Vec<T> v = ldg_vec_nt(x + c * 8);
+  if constexpr (GT > 0) {
+    Vec<T> s[GT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o.e[j] = Elem<T>::st(xf[j] * Elem<T>::ld(s.e[j]));
-    *reinterpret_cast<uint4 *>(xs + ((int64_t)g * chunks + c) * 8) = o.raw;
+    for (int g = 0; g < GT; ++g) s[g] = ldg_vec(sinv + ((int64_t)g * kchunks + kc) * 8);
+    float xf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xf[j] = Elem<T>::ld(v.e[j]);
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      Vec<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.e[j] = Elem<T>::st(xf[j] * Elem<T>::ld(s[g].e[j]));
+      stg_vec_nt(xs + ((int64_t)g * chunks + c) * 8, o);
+    }
+  } else {
+    float xf[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xf[j] = Elem<T>::ld(v.e[j]);
+    for (int g = 0; g < G; ++g) {
+      Vec<T> sv = ldg_vec(sinv + ((int64_t)g * kchunks + kc) * 8);
+      Vec<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.e[j] = Elem<T>::st(xf[j] * Elem<T>::ld(sv.e[j]));
+      stg_vec_nt(xs + ((int64_t)g * chunks + c) * 8, o);
+    }
   }
+}
+
+template <typename T>
+void launch_prescale(const void *x, const void *sinv, void *xs, int64_t M, int64_t K, int G, hipStream_t stream) {
+  const int64_t chunks = M * K / 8;
+  const unsigned gb = (unsigned)((chunks + 255) / 256);
+  const T *xt = reinterpret_cast<const T *>(x);
+  const T *st = reinterpret_cast<const T *>(sinv);
+  T *ot = reinterpret_cast<T *>(xs);
+  if (G == 11)  // alpha_step 0.1, the awq_lite default
+    awq_prescale_kernel<T, 11><<<gb, 256, 0, stream>>>(xt, st, ot, chunks, K / 8, G);
+  else
+    awq_prescale_kernel<T, 0><<<gb, 256, 0, stream>>>(xt, st, ot, chunks, K / 8, G);
 }
 
 // The loss of all G alphas from materialised outputs (the wide linears, whose GEMMs stay on
@@ -919,36 +467,26 @@ __global__ __launch_bounds__(256) void awq_mse_multi_kernel(const T *__restrict_
   if ((int)threadIdx.x < G) partial[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = red[threadIdx.x][0];
 }
 
-// loss[g] += (sum over the group's tiles, in double, fixed order) / (M * N)
+// loss[g] += (sum over the tiles of alpha g, in double, fixed order) / (M * N): one block per
+// alpha (the r03 single block walked the alphas one after another: 28 us per call in the r04 C3
+// profile); per alpha the same summation order as before (per thread strided, then the tree).
 __global__ __launch_bounds__(256) void awq_search_finish_kernel(const float *partial, int tiles, int G,
                                                                  double inv_count, float *loss) {
   __shared__ double red[256];
-  for (int g = 0; g < G; ++g) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < tiles; i += 256) s += (double)partial[(int64_t)g * tiles + i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o >= 1; o >>= 1) {
-      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) loss[g] += (float)(red[0] * inv_count);
+  const int g = blockIdx.x;
+  if (g >= G) return;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < tiles; i += 256) s += (double)partial[(int64_t)g * tiles + i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
+  if (threadIdx.x == 0) loss[g] += (float)(red[0] * inv_count);
 }
 
 bool al16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
-
-// Mode: 2 (default, r03) = pre-scaled activations [G, M, K] in the workspace + the ping-pong
-// kernel (awq_search_pp_kernel); 1 = the r02 kernel with x scaled while register-staged; 0 = the
-// r02 kernel on pre-scaled activations.  r02 measurements (scripts/bench_awq_gemm.py, Llama-3-8B
-// shapes, 8192 tokens, 11 alphas; profiles/r02/awq): mode 1 0.94-0.99 PFLOP/s, mode 0 0.79-1.0
-// including the pre-scale pass -- both at the ceiling of a two-buffer, one-barrier-per-K-step
-// pipeline.  MTQ_AMD_AWQ_GEMM_MODE selects.
-int awq_mode() {  // read per call: A/B runs switch it inside one process
-  const char *e = getenv("MTQ_AMD_AWQ_GEMM_MODE");
-  return e ? atoi(e) : 2;
-}
 
 int64_t partial_floats(int64_t M, int64_t N, int G) {
   return ((((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN) * (int64_t)G) + 3) / 4 * 4;  // 16-B aligned
@@ -958,9 +496,7 @@ int64_t partial_floats(int64_t M, int64_t N, int G) {
 
 extern "C" int64_t mtq_awq_search_gemm_workspace_floats(int64_t M, int64_t N, int64_t K, int G) {
   if (M < 1 || N < 1 || K < 1 || G < 1) return 0;
-  int64_t w = partial_floats(M, N, G);
-  if (awq_mode() != 1) w += (G * M * K + 1) / 2;  // xs [G, M, K] in 16-bit elements
-  return w;
+  return partial_floats(M, N, G) + (G * M * K + 1) / 2;  // + xs [G, M, K] in 16-bit elements
 }
 
 extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const void *bias,
@@ -976,88 +512,34 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
   const int64_t tiles_m = (M + kBM - 1) / kBM, tiles_n = (N + kBN - 1) / kBN;
   const int64_t tiles = tiles_m * tiles_n;
   if (workspace_floats < mtq_awq_search_gemm_workspace_floats(M, N, K, G) ||
-      tiles * G > (int64_t)INT32_MAX)
+      tiles * G > (int64_t)INT32_MAX / 4)
     return MTQ_ERR_INVALID_ARG;
-  const int mode = awq_mode();
-  const bool pre = mode != 1;
-  const void *xa = x;
-  if (pre) {
-    void *xs = workspace + partial_floats(M, N, G);
-    const int64_t chunks = M * K / 8;
-    const unsigned gb = (unsigned)((chunks + 255) / 256);
-    if (dtype == MTQ_BF16)
-      awq_prescale_kernel<__bf16><<<gb, 256, 0, stream>>>((const __bf16 *)x, (const __bf16 *)sinv,
-                                                          (__bf16 *)xs, chunks, K / 8, G);
+  // x * (1/s_g) for every alpha into the workspace (the reference's bf16 multiply, one read of x)
+  void *xs = workspace + partial_floats(M, N, G);
+  if (dtype == MTQ_BF16)
+    launch_prescale<__bf16>(x, sinv, xs, M, K, G, stream);
+  else
+    launch_prescale<_Float16>(x, sinv, xs, M, K, G, stream);
+  int st0 = host_check_launch();
+  if (st0 != MTQ_OK) return st0;
+  AwqGemmArgs a{xs, sinv, wq, bias, yref, workspace, M, N, K, (int)tiles_m, (int)tiles_n, G};
+  // 32 slots per 8 x 4 tile unit, units padded to a multiple of the 8 XCDs (see the kernel)
+  const int64_t units = (int64_t)G * ((tiles_m + 7) / 8) * ((tiles_n + 3) / 4);
+  const dim3 grid((unsigned)((units + 7) / 8 * 8 * 32));
+  if (dtype == MTQ_BF16) {
+    if (bias)
+      awq_search_pp_kernel<__bf16, true><<<grid, kThreads, 0, stream>>>(a);
     else
-      awq_prescale_kernel<_Float16><<<gb, 256, 0, stream>>>((const _Float16 *)x, (const _Float16 *)sinv,
-                                                            (_Float16 *)xs, chunks, K / 8, G);
-    int st = host_check_launch();
-    if (st != MTQ_OK) return st;
-    xa = xs;
-  }
-  AwqGemmArgs a{xa, sinv, wq, bias, yref, workspace, M, N, K, (int)tiles_m, (int)tiles_n, G};
-  const dim3 grid((unsigned)(tiles * G));
-  const char *pe_ = getenv("MTQ_AMD_AWQ_GEMM_PROBE");
-  const int probe = pe_ ? atoi(pe_) : 0;
-#define MTQ_AWQ_LAUNCH(TT, PR)                                                                     \
-  do {                                                                                             \
-    if (probe == 1)                                                                                \
-      awq_search_gemm_kernel<TT, PR, 1><<<grid, kThreads, 0, stream>>>(a);                          \
-    else if (probe == 2)                                                                           \
-      awq_search_gemm_kernel<TT, PR, 2><<<grid, kThreads, 0, stream>>>(a);                          \
-    else                                                                                           \
-      awq_search_gemm_kernel<TT, PR, 0><<<grid, kThreads, 0, stream>>>(a);                          \
-  } while (0)
-  if (mode == 2) {
-    // schedule (A/B switch, profiles/r03/awq): 5 = default; 4 = the first r03 schedule (fragments
-    // re-read per phase; MTQ_AMD_AWQ_PP_CLAMP=0 skips the last tile's loads behind a branch);
-    // 6 = W4, one 128 x 128 wave per SIMD
-    const char *pe = getenv("MTQ_AMD_AWQ_PP_PHASES");
-    const int phs = pe ? atoi(pe) : 5;
-    const char *ce = getenv("MTQ_AMD_AWQ_PP_CLAMP");
-    const bool clamp = ce ? atoi(ce) != 0 : true;
-#define MTQ_PP(TT, BB)                                                                              \
-  do {                                                                                             \
-    if (phs == 6)                                                                                  \
-      awq_search_w4_kernel<TT, BB><<<grid, 256, 0, stream>>>(a);                                    \
-    else if (phs == 4 && probe == 1)                                                               \
-      awq_search_pp_kernel<TT, BB, 4, 1><<<grid, kThreads, 0, stream>>>(a);                         \
-    else if (phs == 4 && !clamp)                                                                   \
-      awq_search_pp_kernel<TT, BB, 4, 0, false><<<grid, kThreads, 0, stream>>>(a);                  \
-    else if (phs == 4)                                                                             \
-      awq_search_pp_kernel<TT, BB, 4><<<grid, kThreads, 0, stream>>>(a);                            \
-    else if (probe == 1)                                                                           \
-      awq_search_pp_kernel<TT, BB, 5, 1><<<grid, kThreads, 0, stream>>>(a);                         \
-    else                                                                                           \
-      awq_search_pp_kernel<TT, BB, 5><<<grid, kThreads, 0, stream>>>(a);                            \
-  } while (0)
-    if (dtype == MTQ_BF16) {
-      if (bias)
-        MTQ_PP(__bf16, true);
-      else
-        MTQ_PP(__bf16, false);
-    } else {
-      if (bias)
-        MTQ_PP(_Float16, true);
-      else
-        MTQ_PP(_Float16, false);
-    }
-#undef MTQ_PP
-  } else if (dtype == MTQ_BF16) {
-    if (pre)
-      MTQ_AWQ_LAUNCH(__bf16, true);
-    else
-      MTQ_AWQ_LAUNCH(__bf16, false);
+      awq_search_pp_kernel<__bf16, false><<<grid, kThreads, 0, stream>>>(a);
   } else {
-    if (pre)
-      awq_search_gemm_kernel<_Float16, true, 0><<<grid, kThreads, 0, stream>>>(a);
+    if (bias)
+      awq_search_pp_kernel<_Float16, true><<<grid, kThreads, 0, stream>>>(a);
     else
-      awq_search_gemm_kernel<_Float16, false, 0><<<grid, kThreads, 0, stream>>>(a);
+      awq_search_pp_kernel<_Float16, false><<<grid, kThreads, 0, stream>>>(a);
   }
-#undef MTQ_AWQ_LAUNCH
   int st = host_check_launch();
   if (st != MTQ_OK) return st;
-  awq_search_finish_kernel<<<1, 256, 0, stream>>>(workspace, (int)tiles, G, 1.0 / ((double)M * (double)N),
+  awq_search_finish_kernel<<<(unsigned)G, 256, 0, stream>>>(workspace, (int)tiles, G, 1.0 / ((double)M * (double)N),
                                                   loss);
   return host_check_launch();
 }
@@ -1085,7 +567,7 @@ extern "C" int mtq_awq_mse_multi(const void *out, const void *ref, int64_t n, in
                                                                       (const _Float16 *)ref, n / 8, G, workspace);
   int st = host_check_launch();
   if (st != MTQ_OK) return st;
-  awq_search_finish_kernel<<<1, 256, 0, stream>>>(workspace, (int)grid, G, 1.0 / (double)n, loss);
+  awq_search_finish_kernel<<<(unsigned)G, 256, 0, stream>>>(workspace, (int)grid, G, 1.0 / (double)n, loss);
   return host_check_launch();
 }
 
@@ -1094,13 +576,9 @@ extern "C" int mtq_awq_prescale(const void *x, const void *sinv, void *xs, int64
   if (M < 1 || K < 8 || K % 8 != 0 || G < 1 || !x || !sinv || !xs) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
   if (!al16(x) || !al16(sinv) || !al16(xs)) return MTQ_ERR_INVALID_ARG;
-  const int64_t chunks = M * K / 8;
-  const unsigned gb = (unsigned)((chunks + 255) / 256);
   if (dtype == MTQ_BF16)
-    awq_prescale_kernel<__bf16><<<gb, 256, 0, stream>>>((const __bf16 *)x, (const __bf16 *)sinv, (__bf16 *)xs,
-                                                        chunks, K / 8, G);
+    launch_prescale<__bf16>(x, sinv, xs, M, K, G, stream);
   else
-    awq_prescale_kernel<_Float16><<<gb, 256, 0, stream>>>((const _Float16 *)x, (const _Float16 *)sinv,
-                                                          (_Float16 *)xs, chunks, K / 8, G);
+    launch_prescale<_Float16>(x, sinv, xs, M, K, G, stream);
   return host_check_launch();
 }
