@@ -1315,21 +1315,36 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   const float span = hi - lo;
   const float y = 1.f / span;
   const uint32_t last = (uint32_t)bins - 1u;
-  for (int p = threadIdx.x; p <= phi; p += kHistValThreads) {
-    const uint32_t c = vh[p];
-    if (c == 0u) continue;
-    const uint16_t bits = (uint16_t)p;
-    T tv;
-    __builtin_memcpy(&tv, &bits, 2);
-    const float a = Elem<T>::ld(tv);
-    if (a <= hi && !(skip_zeros && a == 0.f)) {  // NaN patterns fail the compare
+  // four consecutive patterns per lane (one ds_read_b128, a wave reads 1 KiB contiguous); their
+  // bins are non-decreasing, so the counts of equal bins are summed in registers and leave with
+  // one LDS atomic per run (0.717 -> 0.747 of the HBM roofline on the bench input with the phi
+  // limit above, scripts/exp/hist_exp.hip v41)
+  for (int w = threadIdx.x; w < nz4; w += kHistValThreads) {
+    const uint4 c4 = reinterpret_cast<const uint4 *>(vh)[w];
+    const uint32_t cs[4] = {c4.x, c4.y, c4.z, c4.w};
+    uint32_t run_b = 0xFFFFFFFFu, run_c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * w + j;
+      if (cs[j] == 0u || p > phi) continue;
+      const uint16_t bits = (uint16_t)p;
+      T tv;
+      __builtin_memcpy(&tv, &bits, 2);
+      const float a = Elem<T>::ld(tv);
+      if (!(a <= hi) || (skip_zeros && a == 0.f)) continue;  // NaN patterns fail the compare
       const float t = (a - lo) * fb;
       const float q0 = t * y;
       const float q = __builtin_fmaf(__builtin_fmaf(-q0, span, t), y, q0);
       uint32_t b = (uint32_t)(int)q;
       b = b < last ? b : last;
-      atomicAdd(bh + b, c);
+      if (b != run_b) {
+        if (run_c) atomicAdd(bh + run_b, run_c);
+        run_b = b;
+        run_c = 0;
+      }
+      run_c += cs[j];
     }
+    if (run_c) atomicAdd(bh + run_b, run_c);
   }
   __syncthreads();
   for (int b = threadIdx.x; b < bins; b += kHistValThreads)
@@ -2072,18 +2087,18 @@ __device__ __forceinline__ void export_nvfp4_vec_one(int64_t i, const T *__restr
     st_packed_nt(y + i * (N / 2), (uint16_t)o);
 }
 
-// MXFP4: LPB = block / N lanes per block, shuffle-max, every lane writes N/2 code bytes, the
-// block's first lane its E8M0 byte.
-template <typename T, int BLOCK>
-__device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const T *__restrict__ x,
-                                                                     uint8_t *__restrict__ y,
-                                                                     uint8_t *__restrict__ sc,
-                                                                     int64_t nvec, int native) {
+// MXFP4: LPB = block / N lanes per block, shuffle-max, every lane writes N/2 code bytes.  Scale
+// bytes: with 16-bit elements and block 32 (LPB 4) and a 4-byte aligned scale buffer (SC4), the
+// bytes of 4 consecutive blocks are gathered into lane 16 k of each 16-lane row and leave as one
+// dword store (4 stores per wave instead of 16 single-byte ones); otherwise the block's first lane
+// writes its byte.  The caller loads the lane's vector (all of a thread's loads issued first).
+template <typename T, int BLOCK, bool SC4>
+__device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y,
+                                                     uint8_t *__restrict__ sc, int64_t nvec, int native) {
   using V = Vec<T>;
   constexpr int N = V::N;
   constexpr int LPB = BLOCK / N;
   if (i - (threadIdx.x % LPB) >= nvec) return;
-  V v = ldg_vec_nt(x + i * N);
   float amax = 0.f;
   if constexpr (N == 8) {
     // 16-bit elements: max of the |x| bit patterns, two per packed u16 op (NaN patterns sort
@@ -2115,7 +2130,26 @@ __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const T *__restr
     d6 = amax / 6.0f;
   }
   const float e = mx_e8m0_exponent(d6);
-  if (threadIdx.x % LPB == 0) sc[i / LPB] = (uint8_t)(int)(e + 127.f);
+  const uint32_t sbyte = (uint32_t)(int)(e + 127.f) & 0xFFu;
+  if constexpr (SC4) {
+    static_assert(LPB == 4, "dword scale stores: 4 lanes per block");
+    // lanes 16k .. 16k+15 hold blocks 4k' .. 4k'+3 (vector index i is lane-consecutive and the
+    // chunk base a multiple of 256): gather the three neighbour blocks' bytes into lane 16k
+    const uint32_t b1 = (uint32_t)__shfl_down((int)sbyte, 4, 16);
+    const uint32_t b2 = (uint32_t)__shfl_down((int)sbyte, 8, 16);
+    const uint32_t b3 = (uint32_t)__shfl_down((int)sbyte, 12, 16);
+    if ((threadIdx.x & 15) == 0) {
+      const int64_t blk = i / LPB;
+      if (i + 15 < nvec)
+        __builtin_nontemporal_store(sbyte | (b1 << 8) | (b2 << 16) | (b3 << 24),
+                                    reinterpret_cast<uint32_t *>(sc + blk));
+      else  // the tensor's last, partial row of blocks
+        for (int k = 0; k < 4 && i + 4 * k < nvec; ++k)
+          sc[blk + k] = (uint8_t)(k == 0 ? sbyte : k == 1 ? b1 : k == 2 ? b2 : b3);
+    }
+  } else {
+    if (threadIdx.x % LPB == 0) sc[i / LPB] = (uint8_t)sbyte;
+  }
   uint32_t o = 0;
   if constexpr (N == 8) {
     // Native (16-bit elements, -100 <= e <= 127 so 2^e is a normal scale operand and no input the
@@ -2267,14 +2301,23 @@ __global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__r
   for (int u = 0; u < U; ++u)
     export_nvfp4_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, vpb, fvpb, sblk, s2, native);
 }
-template <int U, typename T, int BLOCK>
+template <int U, typename T, int BLOCK, bool SC4>
 __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__restrict__ x,
                                                                      uint8_t *__restrict__ y,
                                                                      uint8_t *__restrict__ sc,
                                                                      int64_t nvec, int native) {
+  constexpr int LPB = BLOCK / Vec<T>::N;
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  // every load of the thread issued before the first block is converted (the FP8 per-tensor
+  // packer's lesson, 0.589 -> 0.666: a load behind the previous vector's stores was waited for)
+  Vec<T> v[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK>(base + u * kThreads, x, y, sc, nvec, native);
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i - (threadIdx.x % LPB) < nvec) v[u] = ldg_vec_nt(x + i * Vec<T>::N);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK, SC4>(base + u * kThreads, v[u], y, sc, nvec, native);
 }
 
 // U = 2 consecutive 256-vector chunks per block (U = 1 / 4 within run-to-run noise,
@@ -2776,15 +2819,22 @@ int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int 
     constexpr int N = Vec<T>::N;
     if (aligned16(x) && ((uintptr_t)y % (N / 2)) == 0 && (block == 32 || block == 16) && block % N == 0) {
       const int64_t nvec = n / N;
-      if (block == 32)
+      const bool sc4 = N == 8 && block == 32 && ((uintptr_t)scales % 4) == 0;
+      if (block == 32 && sc4)
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
-          export_mxfp4_vec_kernel<U, T, 32><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
+          if constexpr (N == 8)
+            export_mxfp4_vec_kernel<U, T, 32, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
+        });
+      else if (block == 32)
+        with_export_u([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          export_mxfp4_vec_kernel<U, T, 32, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
         });
       else
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
-          export_mxfp4_vec_kernel<U, T, 16><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
+          export_mxfp4_vec_kernel<U, T, 16, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
         });
     } else {
       export_mxfp4_kernel<T><<<grid_for(nb, kThreads), kThreads, 0, stream>>>(

@@ -17,3 +17,8 @@ def test_every_env_switch_is_documented():
     table = design[design.index("## 8b. Environment switches"):design.index("## 9. Status")]
     missing = sorted(u for u in used if u not in table)
     assert not missing, missing
+    # at most 10 switches, each numerics or exercised by a test (the table says which);
+    # no switch documented that the sources no longer read
+    assert len(used) <= 10, sorted(used)
+    documented = set(re.findall(r"`(MTQ_AMD_[A-Z0-9_]+)`", table)) - {"MTQ_AMD_DIST_BACKEND"}
+    assert documented <= used, sorted(documented - used)

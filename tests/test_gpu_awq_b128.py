@@ -106,3 +106,18 @@ def test_awq_lite_fine_alpha_grid_falls_back(gpu):
                 best.setdefault(n, []).append(m.awq_lite.best_alpha)
     for n, b in best.items():
         assert max(b) - min(b) <= 0.0100001, (n, b)
+
+
+def test_awq_lite_without_weight_cache_matches(gpu, monkeypatch):
+    """MTQ_AMD_AWQ_WQ_CACHE_FRACTION = 0: the per-alpha quantised weights are recomputed for every
+    search batch instead of cached across batches (the reference's behaviour) -- the same losses
+    bit for bit, since the cached [G, N, K] tensor is exactly what the recomputation produces."""
+    from modelopt_amd.torch.quantization import model_calib
+
+    cached, _ = _run(gpu, "auto")
+    monkeypatch.setattr(model_calib, "_AWQ_WQ_CACHE_FRACTION", 0.0)
+    fresh, _ = _run(gpu, "auto")
+    for (n, a), (_, b) in zip(cached.named_modules(), fresh.named_modules()):
+        if hasattr(a, "awq_lite"):
+            assert a.awq_lite.loss == b.awq_lite.loss, n
+            assert torch.equal(a.weight, b.weight), n

@@ -105,3 +105,21 @@ def test_histc_thread_count_is_recorded_and_restored(gpu):
         assert torch.equal(f._calibrator._calib_hist.cpu(), t["hist_t1_skip0"])
     finally:
         torch.set_num_threads(saved)
+
+
+def test_histc_exact_counts_mode(gpu, monkeypatch):
+    """MTQ_AMD_HIST_COUNTS=exact: one launch with exact integer counts even when a bin passes 2^24
+    in one call (torch.histc's fp32 counts stop at 2^24 there)."""
+    from hist_inputs import peaked
+    from modelopt_amd.torch.quantization.calib import HistogramCalibrator
+
+    x = peaked(scale=1.0).to(gpu)
+    monkeypatch.setenv("MTQ_AMD_HIST_COUNTS", "exact")
+    h = HistogramCalibrator(8, None, False, num_bins=2048)
+    h.collect(x)
+    got = h._calib_hist.cpu()
+    assert float(got.sum()) == float(x.numel())  # every element counted, no 2^24 saturation
+    assert float(got.max()) > 2**24
+    a = x.float().abs().flatten()
+    want = torch.histc(a.cpu().double(), bins=2048, min=0, max=float(a.max()))
+    assert torch.equal(got.double(), want)

@@ -88,3 +88,13 @@ def test_histc_thread_count_in_quantizer_state():
     m = TensorQuantizer(QuantizerAttributeConfig(num_bits=8))  # max calibrator: the key is ignored
     m.set_from_modelopt_state(state)
     assert not hasattr(m._calibrator, "_histc_threads")
+
+
+def test_hist_threads_env_override(monkeypatch):
+    """MTQ_AMD_HIST_THREADS fixes the chunk count a new histogram calibrator records."""
+    from modelopt_amd.torch.quantization.calib import histogram
+
+    monkeypatch.setenv("MTQ_AMD_HIST_THREADS", "5")
+    assert histogram._histc_threads() == 5
+    monkeypatch.delenv("MTQ_AMD_HIST_THREADS")
+    assert histogram._histc_threads() == max(1, torch.get_num_threads())
