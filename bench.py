@@ -212,6 +212,23 @@ def kernel_suite(ops, xs, steps, warmup):
             "frac": round(gbs / HBM_PEAK_GBS, 4),
             "ms": round(ms, 4),
         }
+    # the calibrator's >2^24-element call ([8192, 14336] = 117.4 M elements, an MLP down_proj
+    # input): torch.histc's per-thread fp32 chunks (16 = the box's CPU share), each counted exactly
+    # and clamped at 2^24, beside one exact-count launch over the same tensor
+    from modelopt_amd.torch.quantization.calib.histogram import _histc_counts  # noqa: PLC0415
+
+    big = [torch.randn(8192, 14336, device="cuda", generator=torch.Generator(device="cuda").manual_seed(7))
+           .to(torch.bfloat16)]
+    nb = big[0].numel()
+    for name, fn in {
+        "histogram_2048_abs_117M_histc16": lambda x: _histc_counts(x, hmax, 2048, False, threads=16),
+        "histogram_2048_abs_117M_exact": lambda x: ops.histogram_abs_accumulate(x, hmax, counts, 2048, False) or counts,
+    }.items():
+        _, ms = time_kernel(fn, big, max(steps // 2, 5), min(warmup, 3))
+        gbs = nb * 2 / (ms * 1e-3) / 1e9
+        res[name] = {"gelem_s": round(nb / (ms * 1e-3) / 1e9, 1), "GB_s": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "ms": round(ms, 4), "elements": nb}
+    del big
     return res
 
 

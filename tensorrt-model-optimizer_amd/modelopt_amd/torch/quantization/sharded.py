@@ -11,8 +11,9 @@ forwards are patched so that
   embeddings / masks, but no decoder compute happens outside the owning rank;
 * the stage's first layer replaces its input with the hidden states received from rank r-1
   (``dist.recv`` -> RCCL point-to-point over xGMI);
-* the stage's last layer sends its output to rank r+1 and ends the forward early (the last rank
-  runs the model's tail normally).
+* the stage's last layer sends its output to rank r+1 with a non-blocking ``isend`` (at most
+  one in flight, waited before the next send) and ends the forward early (the last rank runs the
+  model's tail normally).
 
 Each rank therefore calibrates exactly its own layers' quantizers on the same activations a
 single-GPU run would produce, and consecutive batches overlap across stages (batch i on stage r
@@ -74,11 +75,27 @@ def _is_gloo(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
-def _send(t: torch.Tensor, dst: int, group) -> None:
-    """Point-to-point send (RCCL over xGMI; host-staged under gloo, which has no device P2P)."""
-    if t.device.type != "cpu" and _is_gloo(group):
-        t = t.cpu()
-    dist.send(t, dst=dst, group=group)
+class _Sender:
+    """Non-blocking point-to-point sends (RCCL over xGMI; host-staged under gloo, which has no
+    device P2P).  At most one send is in flight: the next one first waits for the previous, so the
+    stage starts computing batch i+1 while batch i's hidden states are still on the wire and the
+    sent tensor stays alive until its transfer completes."""
+
+    def __init__(self):
+        self._work = None
+        self._tensor = None
+
+    def send(self, t: torch.Tensor, dst: int, group) -> None:
+        if t.device.type != "cpu" and _is_gloo(group):
+            t = t.cpu()
+        self.wait()
+        self._work = dist.isend(t, dst=dst, group=group)
+        self._tensor = t
+
+    def wait(self) -> None:
+        if self._work is not None:
+            self._work.wait()
+        self._work = self._tensor = None
 
 
 def _recv(buf: torch.Tensor, src: int, group) -> None:
@@ -115,6 +132,7 @@ def layer_sharded_calibration(model: nn.Module, plan: LayerShardPlan, group=None
         next_rank = dist.get_global_rank(group, next_rank) if next_rank is not None else None
 
     saved = []
+    sender = _Sender()
 
     def patch(m, fn):
         saved.append((m, m.__dict__.get("forward")))
@@ -139,7 +157,7 @@ def layer_sharded_calibration(model: nn.Module, plan: LayerShardPlan, group=None
             if i == plan.last - 1 and next_rank is not None:
                 if not isinstance(out, torch.Tensor):
                     raise TypeError("layer-sharded calibration needs decoder layers that return a tensor")
-                _send(out.contiguous(), next_rank, group)
+                sender.send(out.contiguous(), next_rank, group)
                 raise _EarlyStopForwardError()
             return out
 
@@ -168,6 +186,7 @@ def layer_sharded_calibration(model: nn.Module, plan: LayerShardPlan, group=None
             if isinstance(m, _qm.QuantModule):
                 m.parallel_state = _qm.ParallelState(data_parallel_group=-1)
         yield plan
+        sender.wait()
     finally:
         _qm._DEFAULT_DP_GROUP = prev_default
         for m, fwd in reversed(saved):

@@ -131,3 +131,32 @@ def test_shard_plan_balanced():
     assert [p.first for p in plans] == list(range(0, 80, 10)) and plans[-1].last == 80
     plans = [layer_shard_plan(10, r, 4) for r in range(4)]
     assert [(p.first, p.last) for p in plans] == [(0, 3), (3, 6), (6, 8), (8, 10)]
+
+
+def test_sender_keeps_one_send_in_flight(monkeypatch):
+    """The stage hand-off is a non-blocking isend: the next send (or the context exit) first waits
+    for the previous transfer, and the sent tensor is held until that wait returns."""
+    import modelopt_amd.torch.quantization.sharded as sh
+
+    log = []
+
+    class _Work:
+        def __init__(self, i):
+            self.i = i
+
+        def wait(self):
+            log.append(("wait", self.i))
+
+    def fake_isend(t, dst, group):
+        log.append(("isend", int(t[0]), dst))
+        return _Work(int(t[0]))
+
+    monkeypatch.setattr(sh.dist, "isend", fake_isend)
+    monkeypatch.setattr(sh, "_is_gloo", lambda g: True)
+    s = sh._Sender()
+    s.send(torch.tensor([1.0]), 1, None)
+    assert log == [("isend", 1, 1)] and s._tensor is not None
+    s.send(torch.tensor([2.0]), 1, None)
+    assert log == [("isend", 1, 1), ("wait", 1), ("isend", 2, 1)]
+    s.wait()
+    assert log[-1] == ("wait", 2) and s._tensor is None and s._work is None
