@@ -146,6 +146,18 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
 int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                       int skip_zeros, uint32_t *counts, hipStream_t stream);
 
+/* torch.histc's CPU accumulation for calls above 2^24 elements (calib/histogram.py:116-130 ->
+ * torch.histc -> at::parallel_for): element chunk c is [bounds[c], bounds[c+1]) (device int64
+ * [chunks + 1], e.g. the skip_zeros boundaries mapped back to the input), or, with bounds null,
+ * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  Each chunk is counted exactly in one launch
+ * into its row of `scratch` (uint32 [chunks, bins], zeroed here), then
+ * hist[b] = sum_c min(fp32(scratch[c][b]), 2^24) in chunk order (overwritten, fp32 [bins]).
+ * bf16 / f16 only, x 16-byte aligned, n % 8 == 0, bins <= 8192 (MTQ_ERR_DTYPE /
+ * MTQ_ERR_INVALID_ARG otherwise: the caller counts chunk by chunk with mtq_histogram_abs). */
+int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
+                              int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
+                              uint32_t *scratch, float *hist, hipStream_t stream);
+
 /* ---- NVFP4 --------------------------------------------------------------------------------
  * Two-level dynamic NVFP4 fake quant of x [rows, cols] (blocks of block_size along cols, zero
  * padded): the reference's primary NVFP4 kernel, fp4_fake_quant_block

@@ -41,7 +41,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, uint
 // SAME alpha and n-range, different m-groups: every W panel is fetched from HBM once and shared
 // through the Infinity Cache, the alpha's activations stay resident there.  Slots past the
 // matrix edge exit at once.
-template <int PROBE, int GM, int BUF, int MAP = 0>
+// YPF 1: the reference (yref) tile of the epilogue rides in the K loop's past-the-end half-loads
+// (tile nt-2 phases 2-3 and tile nt-1 phases 0-3 re-load clamped K tiles nobody reads): each such
+// half writes the same 16 KiB of LDS the yref rounds 2 b + {0, 1} (b = its 8 KiB index) occupy in
+// the epilogue layout, at the same time as the re-load would have -- same WAR margins, same DMA
+// count for the counted waits -- so 12 of the tile's 16 rounds are in flight before the loop ends
+// and only the last buffer's A1 / B1 slots (4 rounds) load after it.  YPF 2: no yref load at all
+// (probe: the epilogue's load cost; loss wrong).
+template <int PROBE, int GM, int BUF, int MAP = 0, int YPF = 0>
 __global__ __launch_bounds__(kThreads) void pp_exp_kernel(Args p) {
   typedef __bf16 v8 __attribute__((ext_vector_type(8)));
   __shared__ __attribute__((aligned(16))) unsigned char lds[kLds];
@@ -112,6 +119,23 @@ __global__ __launch_bounds__(kThreads) void pp_exp_kernel(Args p) {
       }
     }
   };
+  const __bf16 *Y = reinterpret_cast<const __bf16 *>(p.yref);
+  auto yref_round = [&](int r) {  // 16 rows x 256 columns of yref -> LDS bytes [r * 8 KiB, +8 KiB)
+    const int rr = r * 16 + (tid >> 5);
+    int64_t row = m0 + rr;
+    row = row < p.M ? row : p.M - 1;
+    int64_t col = n0 + (int64_t)(((tid & 31) ^ (rr & 15)) * 8);
+    col = col < p.N ? col : p.N - 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
+                                     (__attribute__((address_space(3))) void *)(lds + r * 8192 + wave * 1024), 16, 0, 0);
+  };
+  auto load_yref_half = [&](int q, unsigned char *buf) {
+    const bool isA = (q == 0 || q == 3);
+    const int h = (q == 0 || q == 1) ? 0 : 1;
+    const int r0 = (int)((buf - lds) / 8192) + (isA ? h : 2 + h) * 2;
+    yref_round(r0);
+    yref_round(r0 + 1);
+  };
   const int sw = (lane >> 1) & 7, fr = lane & 15, fq = lane >> 4;
   auto read_a = [&](const unsigned char *buf, int i, int s) -> v8 {
     const int L = (i >> 2) * 128 + grp * 64 + (i & 3) * 16 + fr;
@@ -171,7 +195,10 @@ __global__ __launch_bounds__(kThreads) void pp_exp_kernel(Args p) {
       unsigned char *hb = q < 2 ? nx1 : cur;
       const int64_t hk = q < 2 ? k1 : k2;
       if (PROBE != 1) {
-        load_half(hq, hb, hk);
+        if (YPF == 1 && nt >= 2 && (q < 2 ? t + 1 >= nt : t + 2 >= nt))
+          load_yref_half(hq, hb);
+        else
+          load_half(hq, hb, hk);
         if (q == 2)
           wait_vm<10>();
         else
@@ -193,23 +220,19 @@ __global__ __launch_bounds__(kThreads) void pp_exp_kernel(Args p) {
   if (grp == 0) __builtin_amdgcn_s_barrier();
   // epilogue as the product kernel (no bias): the loss partial
   float sum = 0.f;
-  const __bf16 *Y = reinterpret_cast<const __bf16 *>(p.yref);
   typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
   u32x2_t yv[8][4];
   wait_vm<0>();
   __syncthreads();
-  {
-    const int slot = tid & 31;
+  if (YPF == 1 && nt >= 2) {
+    const int b = ((nt - 1) & 1) * 8;  // the last K tile's A1 / B1 slots
+    yref_round(b + 2);
+    yref_round(b + 3);
+    yref_round(b + 6);
+    yref_round(b + 7);
+  } else if (YPF != 2) {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int rr = u * 16 + (tid >> 5);
-      int64_t row = m0 + rr;
-      row = row < p.M ? row : p.M - 1;
-      int64_t col = n0 + (int64_t)((slot ^ (rr & 15)) * 8);
-      col = col < p.N ? col : p.N - 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(Y + row * p.N + col),
-                                       (__attribute__((address_space(3))) void *)(lds + u * 8192 + wave * 1024), 16, 0, 0);
-    }
+    for (int u = 0; u < 16; ++u) yref_round(u);
   }
   wait_vm<0>();
   __syncthreads();
@@ -248,14 +271,14 @@ __global__ __launch_bounds__(kThreads) void pp_exp_kernel(Args p) {
   }
 }
 
-template <int PROBE, int GM, int BUF, int MAP = 0>
+template <int PROBE, int GM, int BUF, int MAP = 0, int YPF = 0>
 int go(const Args &a, hipStream_t stream) {
   unsigned grid = (unsigned)(a.tiles_m * a.tiles_n * a.G);
   if (MAP == 1) {
     const int units = a.G * ((a.tiles_m + 7) / 8) * ((a.tiles_n + 3) / 4);
     grid = (unsigned)((units + 7) / 8 * 8 * 32);
   }
-  pp_exp_kernel<PROBE, GM, BUF, MAP><<<grid, kThreads, 0, stream>>>(a);
+  pp_exp_kernel<PROBE, GM, BUF, MAP, YPF><<<grid, kThreads, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -476,6 +499,8 @@ extern "C" int awq_exp(int var, const void *xs, const void *wq, const void *yref
   case 30: return go<0, 8, 0, 1>(a, stream);
   case 31: return go<0, 8, 1, 1>(a, stream);
   case 33: return go<3, 8, 0, 1>(a, stream);
+  case 34: return go<0, 8, 1, 1, 1>(a, stream);
+  case 35: return go<0, 8, 1, 1, 2>(a, stream);
   case 50: return go_ring<0>(a, stream);
   case 53: return go_ring<3>(a, stream);
   default: return 3;

@@ -20,7 +20,7 @@ ops = _ext.ops()
 lib = ctypes.CDLL(str(REPO / "scripts/exp/libawq_exp.so"))
 lib.awq_exp.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
-VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "31,33,50,53".split(","))]
+VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "31,34,35,50,53".split(","))]
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 SHAPES = {"q_proj": (4096, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
 M, G = 8192, 11
@@ -59,7 +59,7 @@ for name, (N, K) in SHAPES.items():
     # correctness of the copy: variant 0's per-alpha loss equals the product's
     l0 = torch.zeros(G, device=dev)
     ops.awq_search_gemm(x, si, wq, None, yref, l0)
-    for v in [0] + [v for v in VARS if v in (10, 20, 21, 22, 30, 31, 50)]:
+    for v in [0] + [v for v in VARS if v in (10, 20, 21, 22, 30, 31, 34, 50)]:
         part.fill_(float("nan"))
         var(v)()
         torch.cuda.synchronize()

@@ -32,6 +32,7 @@ acc = torch.zeros(1, device="cuda")
 hmax = torch.tensor([16.0 * 6], device="cuda")  # bench.py's histogram range
 counts = torch.zeros(2048, dtype=torch.int32, device="cuda")
 nv_bs = torch.ones(T, H // 16, device="cuda")  # bench.py's export_nvfp4_pack scales
+i4_s = torch.full((T, H // 128), 0.01, device="cuda")  # bench.py's export_int4_pack scales
 torch.cuda.synchronize()
 for i in range(args.iters):
     x = xs[i % 4]
@@ -53,6 +54,8 @@ for i in range(args.iters):
         ops.export_fp8(x, amax / 448, False, True)
     elif args.kernel == "export_nvfp4":
         ops.export_nvfp4(x, nv_bs, amax / 2688)
+    elif args.kernel == "export_int4":
+        ops.export_int4(x, i4_s)
     elif args.kernel == "export_mxfp4":
         ops.export_mxfp4(x, 32)
     else:

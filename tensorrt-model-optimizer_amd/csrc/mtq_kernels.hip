@@ -1225,10 +1225,22 @@ __global__ __launch_bounds__(kHistDivThreads) void hist_div_kernel(
 // bins, so one 1024-thread block per CU over one contiguous chunk.
 constexpr int kHistValThreads = 1024;
 constexpr int kHistPatterns = 32768;
-template <typename T, int U, bool PF>
+//
+// CHUNKED: the torch.histc chunk emulation in one launch.  Chunk c covers elements [e0, e1) (from
+// `bounds`, or c * chunk_elems clipped to n_elems when bounds is null) and owns `bpc` consecutive
+// blocks and the count row counts[c * bins, +bins); element bounds need not fall on vectors, so
+// the two edge vectors of a chunk mask their out-of-chunk halves to the dropped NaN pattern.
+struct HistChunks {
+  const int64_t *bounds;  // [chunks + 1] element offsets (device), or null: uniform chunks
+  int64_t chunk_elems;
+  int64_t n_elems;
+  int bpc;  // blocks per chunk
+};
+
+template <typename T, int U, bool PF, bool CHUNKED = false>
 __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
     const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
-    int skip_zeros, uint32_t *counts) {
+    int skip_zeros, uint32_t *counts, HistChunks ch) {
   static_assert(sizeof(T) == 2, "pattern histogram is for 16-bit floats");
   extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
   uint32_t *vh = sh;                  // [32768] counts per |x| bit pattern
@@ -1260,9 +1272,29 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   for (int i = threadIdx.x; i < nz4; i += kHistValThreads)
     reinterpret_cast<uint4 *>(vh)[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int b = threadIdx.x; b < bins; b += kHistValThreads) bh[b] = 0;
-  const int64_t v0 = (int64_t)blockIdx.x * vec_per_block;
-  int64_t v1 = v0 + vec_per_block;
-  v1 = v1 < nvec ? v1 : nvec;
+  int64_t v0, v1, e0 = 0, e1 = 0;
+  if constexpr (CHUNKED) {
+    const int c = blockIdx.x / ch.bpc, s = blockIdx.x % ch.bpc;
+    if (ch.bounds) {
+      e0 = ch.bounds[c];
+      e1 = ch.bounds[c + 1];
+    } else {
+      e0 = (int64_t)c * ch.chunk_elems;
+      e0 = e0 < ch.n_elems ? e0 : ch.n_elems;
+      e1 = e0 + ch.chunk_elems;
+      e1 = e1 < ch.n_elems ? e1 : ch.n_elems;
+    }
+    const int64_t cv0 = e0 / 8, cv1 = (e1 + 7) / 8;
+    const int64_t per = (cv1 - cv0 + ch.bpc - 1) / ch.bpc;
+    v0 = cv0 + (int64_t)s * per;
+    v1 = v0 + per;
+    v1 = v1 < cv1 ? v1 : cv1;
+    counts += (int64_t)c * bins;
+  } else {
+    v0 = (int64_t)blockIdx.x * vec_per_block;
+    v1 = v0 + vec_per_block;
+    v1 = v1 < nvec ? v1 : nvec;
+  }
   constexpr int64_t kStep = (int64_t)kHistValThreads * U;
   // one U-vector batch per lane; past-the-end slots read as a NaN pattern (dropped by the fold)
   auto load = [&](int64_t i, uint4 (&v)[U]) {
@@ -1272,6 +1304,17 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
       if (k < v1) {
         const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + k * 8));
         v[u] = make_uint4(r.x, r.y, r.z, r.w);
+        if constexpr (CHUNKED) {
+          if (k * 8 < e0 || k * 8 + 8 > e1) {  // a chunk's edge vector: drop the outside halves
+            uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int64_t e = k * 8 + j;
+              if (e < e0 || e >= e1) w[j / 2] |= 0x7FFFu << (16 * (j % 2));
+            }
+            v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        }
       } else {
         v[u] = make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
       }
@@ -1774,7 +1817,10 @@ __device__ __forceinline__ float mx_e8m0_exponent(float d) {
   float e;
   if (((b >> 23) & 0xff) != 0 && m == 0) {
     e = (float)ex;
-  } else if (((b >> 23) & 0xff) != 0 && m > (1u << 13)) {
+  } else if (((b >> 23) & 0xff) != 0 && m > 64u) {
+    // log2(d) = ex + log2(1 + m 2^-23) rounds above ex for every normal d with m > 64 (the largest
+    // m that rounds back to ex is 22: scripts/check_e8m0.c, exhaustive), so ceil gives ex + 1 --
+    // the double-precision log2 below runs for 1 block in 2^17 instead of 1 in 2^10
     e = (float)(ex + 1);
   } else {
     e = __builtin_ceilf((float)log2((double)d));
@@ -2254,8 +2300,10 @@ __global__ __launch_bounds__(kThreads) void export_fp8_pt_kernel(const T *__rest
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
   Vec<T> v[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (base + u * kThreads < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * Vec<T>::N);
+  for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: see export_mxfp4_vec_kernel
+    const int64_t i = base + u * kThreads;
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * Vec<T>::N);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
     if (base + u * kThreads < nvec) export_fp8_pt_one<T, ROUND>(base + u * kThreads, v[u], y, s, r);
@@ -2310,11 +2358,16 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
   // every load of the thread issued before the first block is converted (the FP8 per-tensor
   // packer's lesson, 0.589 -> 0.666: a load behind the previous vector's stores was waited for)
+  // The loads are unconditional (a lane past the end re-reads the last vector, n % block == 0 so
+  // whole blocks are past it and export_mxfp4_vec_one drops them): a load under a lane condition
+  // made the compiler wait vmcnt(0) right behind each one (the wait analysis is path-insensitive),
+  // serialising the U loads.
+  static_assert(LPB >= 1, "block holds whole vectors");
   Vec<T> v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kThreads;
-    if (i - (threadIdx.x % LPB) < nvec) v[u] = ldg_vec_nt(x + i * Vec<T>::N);
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * Vec<T>::N);
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK, SC4>(base + u * kThreads, v[u], y, sc, nvec, native);
@@ -2564,7 +2617,8 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
           attr = true;
         }
-        kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins, skip_zeros, counts);
+        kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins, skip_zeros, counts,
+                                                                    HistChunks{});
         return check_launch();
       }
     }
@@ -2600,6 +2654,57 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
     unsigned g = grid_for(n, kThreads * 8);
     hist_kernel<T><<<g, kThreads, shm, stream>>>(xt, n, hmax, bins, skip_zeros, counts, lds ? 1 : 0);
     return check_launch();
+  });
+}
+
+// hist[b] = sum over chunks c, in chunk order, of min(fp32(counts[c][b]), 2^24): torch.histc's
+// per-thread fp32 histograms (a counter stops at 2^24) added in thread order
+__global__ __launch_bounds__(kThreads) void hist_chunk_sum_kernel(const uint32_t *__restrict__ counts,
+                                                                  int chunks, int bins,
+                                                                  float *__restrict__ hist) {
+  const int b = blockIdx.x * kThreads + threadIdx.x;
+  if (b >= bins) return;
+  float h = 0.f;
+  for (int c = 0; c < chunks; ++c) h += fminf((float)counts[(int64_t)c * bins + b], 16777216.f);
+  hist[b] = h;
+}
+
+int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
+                              int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
+                              uint32_t *scratch, float *hist, hipStream_t stream) {
+  if (n < 0 || bins < 1 || bins > 8192 || chunks < 1 || !hmax || !scratch || !hist || (n > 0 && !x))
+    return MTQ_ERR_INVALID_ARG;
+  if (!bounds && (chunk_elems < 1 || (chunks - 1) * chunk_elems >= n)) return MTQ_ERR_INVALID_ARG;
+  if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
+  if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
+  if (hipMemsetAsync(scratch, 0, (size_t)chunks * bins * 4, stream) != hipSuccess) return MTQ_ERR_LAUNCH;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    if constexpr (sizeof(T) == 2) {
+      // ~one 1024-thread block per CU in total, at least kHistValThreads * 8 vectors per block
+      const int64_t cvec = (n / 8 + chunks - 1) / chunks;
+      int64_t bpc = ((int64_t)num_cus() + chunks - 1) / chunks;
+      const int64_t by_size = (cvec + (int64_t)kHistValThreads * 8 - 1) / ((int64_t)kHistValThreads * 8);
+      bpc = bpc < by_size ? bpc : by_size;
+      bpc = bpc < 1 ? 1 : bpc;
+      if ((int64_t)chunks * bpc > INT32_MAX) return MTQ_ERR_INVALID_ARG;
+      const size_t shr = ((size_t)kHistPatterns + (size_t)bins) * 4;
+      auto kern = hist_value_kernel<T, 2, true, true>;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      const HistChunks ch{bounds, chunk_elems, n, (int)bpc};
+      kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
+                                                                      hmax, bins, skip_zeros, scratch, ch);
+      if (check_launch() != MTQ_OK) return MTQ_ERR_LAUNCH;
+      hist_chunk_sum_kernel<<<(unsigned)((bins + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+          scratch, chunks, bins, hist);
+      return check_launch();
+    }
+    return MTQ_ERR_DTYPE;
   });
 }
 

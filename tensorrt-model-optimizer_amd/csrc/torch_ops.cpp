@@ -870,6 +870,33 @@ void histogram_abs_accumulate(const at::Tensor &inputs, const at::Tensor &hmax, 
   check_status(st, "histogram_abs");
 }
 
+at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hmax, int64_t bins,
+                                 bool skip_zeros, const c10::optional<at::Tensor> &bounds,
+                                 int64_t chunk_elems, int64_t chunks) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  TORCH_CHECK(hmax.scalar_type() == at::kFloat && hmax.numel() == 1, "histogram: hmax fp32 scalar");
+  TORCH_CHECK(chunks >= 1 && chunks <= (1 << 20), "histogram_abs_chunked: bad chunk count");
+  const int64_t *bp = nullptr;
+  at::Tensor b;
+  if (bounds.has_value() && bounds->defined()) {
+    b = bounds->contiguous();
+    TORCH_CHECK(b.scalar_type() == at::kLong && b.numel() == chunks + 1 && b.device() == x.device(),
+                "histogram_abs_chunked: bounds must be int64 [chunks + 1] on the input's device");
+    bp = b.data_ptr<int64_t>();
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor scratch = at::empty({chunks, bins}, x.options().dtype(at::kInt));
+  at::Tensor hist = at::empty({bins}, x.options().dtype(at::kFloat));
+  int st = mtq_histogram_abs_chunked(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"),
+                                     hmax.data_ptr<float>(), (int)bins, skip_zeros ? 1 : 0, bp,
+                                     chunk_elems, (int)chunks,
+                                     reinterpret_cast<uint32_t *>(scratch.data_ptr<int32_t>()),
+                                     hist.data_ptr<float>(), cur_stream(x));
+  check_status(st, "histogram_abs_chunked");
+  return hist;
+}
+
 // ---- reference torch.library ops (tensor_quant.py:115-195) -------------------------------------
 at::Tensor quantize_op(const at::Tensor &input, const at::Tensor &amax, int64_t num_bits,
                        int64_t exponent_bits, bool is_unsigned, bool narrow_range) {
@@ -1000,6 +1027,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
         "bool unsigned, bool narrow_range) -> Tensor");
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
         "bool skip_zeros) -> ()");
+  m.def("histogram_abs_chunked(Tensor inputs, Tensor hmax, int bins, bool skip_zeros, Tensor? bounds, "
+        "int chunk_elems, int chunks) -> Tensor");
   m.def("qlinear_small_m_group(Tensor[] inputs, Tensor[] weights, Tensor?[] biases, Tensor[] amaxs, int[] blocks, "
         "int kind, int[] num_bits, int[] is_unsigned, int[] narrow_range) -> Tensor[]");
   m.def("qlinear_small_m(Tensor input, Tensor weight, Tensor? bias, Tensor amax, int block, int kind, "
@@ -1044,6 +1073,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("amax_accumulate", &amax_accumulate);
   m.impl("block_quant_dynamic", &block_quant_dynamic);
   m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);
+  m.impl("histogram_abs_chunked", &histogram_abs_chunked);
   m.impl("mse_accumulate", &mse_accumulate);
   m.impl("mul_cols", &mul_cols);
   m.impl("awq_search_gemm", &awq_search_gemm);

@@ -155,8 +155,8 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     Every count of a call with at most 2^24 (kept) elements is exact in fp32 whatever the chunking,
     so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T = threads``,
     default ``_histc_threads()``; chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted
-    by its own launch (exact integers), clamped at 2^24 and added into the fp32 result in thread
-    order."""
+    exactly, clamped at 2^24 and added into the fp32 result in thread order: bf16 / f16 on the GPU
+    in two launches for all chunks (histogram_abs_chunked), other inputs one launch per chunk."""
     ops = _ops()
     n = x.numel()
     mode = os.environ.get("MTQ_AMD_HIST_COUNTS", "histc")
@@ -178,12 +178,20 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     threads = min(threads or _histc_threads(), -(-kept // _HISTC_GRAIN))
     chunk = -(-kept // threads)
     starts = [t * chunk for t in range(threads) if t * chunk < kept] + [kept]
+    cuts = None
     if csum is not None:
         # the first original index whose non-zero rank reaches each compacted start
         cuts = torch.searchsorted(csum, torch.tensor(starts[1:-1], device=csum.device, dtype=torch.int64) + 1)
-        bounds = [0] + cuts.tolist() + [n]
-    else:
-        bounds = starts
+    if (flat.is_cuda and flat.dtype in (torch.bfloat16, torch.float16) and bins <= 8192 and n % 8 == 0
+            and flat.data_ptr() % 16 == 0):
+        # one launch counts every chunk into its own row, a second adds the clamped rows in order
+        nch = len(starts) - 1
+        dev_bounds = None
+        if cuts is not None:
+            z = torch.zeros(1, dtype=torch.int64, device=flat.device)
+            dev_bounds = torch.cat([z, cuts, torch.full_like(z, n)])
+        return ops.histogram_abs_chunked(flat, hmax, bins, skip_zeros, dev_bounds, chunk, nch)
+    bounds = [0] + cuts.tolist() + [n] if cuts is not None else starts
     hist = torch.zeros(bins, dtype=torch.float32, device=x.device)
     counts = torch.empty(bins, dtype=torch.int32, device=x.device)
     for b, e in zip(bounds[:-1], bounds[1:]):

@@ -47,3 +47,18 @@ def test_mxfp4_block_scale_division_matches_ieee(tmp_path):
     )
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("mismatches 0"), r.stdout
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_e8m0_exponent_shortcut(tmp_path):
+    """mx_e8m0_exponent's fast path (mantissa > 64 -> ex + 1) equals ceil(fp32(log2(d)))
+    (qtensor/mxfp4_tensor.py:62-66); strided slice of scripts/check_e8m0.c (stride 1 recorded in
+    DESIGN §5)."""
+    exe = tmp_path / "chk_e8m0"
+    subprocess.run(
+        ["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(REPO / "scripts" / "check_e8m0.c"), "-lm"],
+        check=True,
+    )
+    r = subprocess.run([str(exe), "61"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
+    assert "mismatches 0" in r.stdout and "needing log2: 22" in r.stdout, r.stdout

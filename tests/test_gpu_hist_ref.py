@@ -123,3 +123,45 @@ def test_histc_exact_counts_mode(gpu, monkeypatch):
     a = x.float().abs().flatten()
     want = torch.histc(a.cpu().double(), bins=2048, min=0, max=float(a.max()))
     assert torch.equal(got.double(), want)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_histc_chunked_single_launch_matches_per_chunk_counts(gpu, dtype):
+    """histogram_abs_chunked (every chunk in one launch, rows summed in chunk order) against the
+    per-chunk launches over slices: chunk edges off the 8-element vectors, uniform and explicit
+    (skip_zeros-style) bounds, 1..16 chunks, a bin past 2^24 in the sum."""
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    g = torch.Generator(device=gpu).manual_seed(3)
+    n = 8 * 2_100_003
+    x = (torch.randn(n, device=gpu, generator=g) * 2).to(dtype)
+    x[::5] = 0
+    x[7::11] = 0.25  # one heavy bin
+    hmax = torch.tensor([6.0], device=gpu)
+    F32 = 2**24
+
+    def per_chunk(bounds, skip):
+        h = torch.zeros(2048, device=gpu)
+        for b, e in zip(bounds[:-1], bounds[1:]):
+            c = torch.zeros(2048, dtype=torch.int32, device=gpu)
+            if e > b:
+                ops.histogram_abs_accumulate(x[b:e], hmax, c, 2048, skip)
+            h += c.float().clamp_(max=F32)
+        return h
+
+    for chunks in (1, 3, 16):
+        chunk = -(-n // chunks)
+        bounds = [min(t * chunk, n) for t in range(chunks)] + [n]
+        for skip in (False, True):
+            got = ops.histogram_abs_chunked(x, hmax, 2048, skip, None, chunk, chunks)
+            assert torch.equal(got, per_chunk(bounds, skip)), (chunks, skip)
+    # explicit device bounds, ragged (including an empty chunk)
+    bounds = [0, 13, 13, 1_000_001, 9_999_999, n - 3, n]
+    dev_b = torch.tensor(bounds, dtype=torch.int64, device=gpu)
+    got = ops.histogram_abs_chunked(x, hmax, 2048, True, dev_b, 0, len(bounds) - 1)
+    assert torch.equal(got, per_chunk(bounds, True))
+    # 2^24 clamp: a single chunk holding > 2^24 elements of the heavy bin
+    y = torch.full((F32 + 64,), 0.25, dtype=dtype, device=gpu)
+    got = ops.histogram_abs_chunked(y, hmax, 2048, False, None, F32 + 64, 1)
+    assert float(got.max()) == float(F32) and float(got.sum()) == float(F32)
