@@ -566,8 +566,10 @@ __global__ __launch_bounds__(kThreads) void mx_vec_kernel(const T *__restrict__ 
   const int lead = threadIdx.x % LPB;
   V v[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (base + u * kThreads - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * N);
+  for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: see export_mxfp4_vec_kernel
+    const int64_t i = base + u * kThreads;
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * N);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kThreads;
@@ -859,15 +861,17 @@ __global__ __launch_bounds__(kThreads) void amax_rows_u_kernel(const T *__restri
   int64_t v1 = v0 + G * U;
   v1 = v1 < qvec ? v1 : qvec;
   const T *row = x + r * Q;
+  // unconditional loads (a lane past the chunk re-reads its last vector, then contributes 0): a
+  // load under a lane condition is waited with vmcnt(0) right behind it, serialising the U loads
   V v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = v0 + gl + u * G;
-    if (i < v1)
-      v[u] = ldg_vec_nt(row + i * N);
-    else
-      v[u].raw = make_uint4(0, 0, 0, 0);
+    v[u] = ldg_vec_nt(row + (i < v1 ? i : v1 - 1) * N);
   }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (v0 + gl + u * G >= v1) v[u].raw = make_uint4(0, 0, 0, 0);
   uint32_t m = 0;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -995,12 +999,13 @@ __global__ __launch_bounds__(kThreads) void amax_rows_short_kernel(const T *__re
   }
   V v[RU];
 #pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    if (r0 + u < R && gl < qvec)
-      v[u] = ldg_vec_nt(x + (r0 + u) * Q + (int64_t)gl * N);
-    else
-      v[u].raw = make_uint4(0, 0, 0, 0);
+  for (int u = 0; u < RU; ++u) {  // unconditional (clamped) loads, as amax_rows_u_kernel
+    const int64_t rr = r0 + u < R ? r0 + u : R - 1;
+    v[u] = ldg_vec_nt(x + rr * Q + (int64_t)(gl < qvec ? gl : qvec - 1) * N);
   }
+#pragma unroll
+  for (int u = 0; u < RU; ++u)
+    if (!(r0 + u < R && gl < qvec)) v[u].raw = make_uint4(0, 0, 0, 0);
 #pragma unroll
   for (int u = 0; u < RU; ++u) {
     uint32_t m = group_max_u32<G>(vec_absmax_bits(v[u]));
@@ -1093,8 +1098,10 @@ __global__ __launch_bounds__(kThreads) void block_quant_dyn_kernel(
   const int lead = threadIdx.x % LPB;  // a block's LPB lanes are in range together
   V v[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (base + u * kThreads - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * N);
+  for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: see export_mxfp4_vec_kernel
+    const int64_t i = base + u * kThreads;
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * N);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kThreads;
@@ -2295,8 +2302,6 @@ __global__ __launch_bounds__(kThreads) void export_fp8_pt_kernel(const T *__rest
                                                                   uint8_t *__restrict__ y,
                                                                   int64_t nvec,
                                                                   const float *__restrict__ scale) {
-  const float s = scale[0];
-  const float r = 1.0f / s;
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
   Vec<T> v[U];
 #pragma unroll
@@ -2304,9 +2309,21 @@ __global__ __launch_bounds__(kThreads) void export_fp8_pt_kernel(const T *__rest
     const int64_t i = base + u * kThreads;
     v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * Vec<T>::N);
   }
+  // the scale after the data loads (the empty asm keeps the compiler from hoisting its scalar
+  // load and wait above them): its round trip and 1/s overlap the data's
+  asm volatile("" ::: "memory");
+  const float s = scale[0];
+  const float r = 1.0f / s;
+  // a whole block in range (all but the last) converts unconditionally: with only the lane-guarded
+  // form the compiler sank the first load into its guarded consumer and waited vmcnt(0) there
+  if ((int64_t)(blockIdx.x + 1) * (kThreads * U) <= nvec) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (base + u * kThreads < nvec) export_fp8_pt_one<T, ROUND>(base + u * kThreads, v[u], y, s, r);
+    for (int u = 0; u < U; ++u) export_fp8_pt_one<T, ROUND>(base + u * kThreads, v[u], y, s, r);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * kThreads < nvec) export_fp8_pt_one<T, ROUND>(base + u * kThreads, v[u], y, s, r);
+  }
 }
 
 template <int U, typename T, bool IDX32>
