@@ -9,23 +9,15 @@
 //
 //     loss[g] += mean_{m,n} float(T(T(sum_k T(x[m,k] * sinv[g,k]) * wq[g,n,k] + b[n]) - yref[m,n]))^2
 //
-// with the x * (1/s) product (rounded to T as the reference's bf16 multiply is) applied while the
-// A tile is staged into LDS, bf16/f16 MFMA (v_mfma_f32_32x32x16, fp32 accumulate), and the bias,
-// output rounding, difference (rounded to T, as the reference's subtraction) and square-sum done
-// on the accumulators -- out never reaches HBM.  wq[g] = qdq_int4_b128(W * s_g) comes from
-// mtq_block_quant_dynamic (one HBM pass per alpha).  Grouping the alphas in one grid (tile x g)
-// also fills the 256 CUs for the narrow linears (k/v_proj: 4 x 32 tiles per alpha).
-//
-// Tiling: 256 x 256 output tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 per
-// wave = 4 x 2 tiles of 32 x 32), K step 64, LDS double-buffered (2 x (32 + 32) KiB in one
-// __shared__ array).  W tile: global_load_lds (16 B per lane) straight into LDS; x tile: register
-// staged (global_load_dwordx4 -> scale by sinv -> ds_write_b128), the next tile's loads issued
-// before the current tile's MFMAs.  LDS rows are 128 B; the 16-byte chunk c of row r sits at
-// chunk c ^ ((r >> 1) & 7) so the 16-lane groups of every ds_read_b128 hit 16 distinct bank
-// slots (cdna_hip_programming.md T2; for the glds-filled W tile the swizzle is applied to the
-// global source address, rule 21).  Workgroups are remapped so each XCD runs a contiguous range
-// of tiles (T1).  The loss is summed per lane in fp32 in a fixed order, across the workgroup in a
-// fixed order, and the per-tile partials are folded in double by a one-block finishing kernel:
+// with the x * (1/s) product (rounded to T as the reference's bf16 multiply is) written once for
+// all alphas by awq_prescale_kernel, bf16/f16 MFMA (v_mfma_f32_16x16x32, fp32 accumulate), and
+// the bias, output rounding, difference (rounded to T, as the reference's subtraction) and
+// square-sum done on the accumulators -- out never reaches HBM.  wq[g] = qdq_int4_b128(W * s_g)
+// comes from mtq_block_quant_dynamic_multi (one HBM pass for all alphas).  Grouping the alphas in
+// one grid (tile x g) also fills the 256 CUs for the narrow linears (k/v_proj: 4 x 32 tiles per
+// alpha).  The search kernel (awq_search_pp_kernel below) describes its tiling and schedule; the
+// loss is summed per lane in fp32 in a fixed order, across the workgroup in a fixed order, and
+// the per-tile partials are folded in double by a one-block-per-alpha finishing kernel:
 // deterministic run to run.
 #include <hip/hip_runtime.h>
 #include <stdint.h>

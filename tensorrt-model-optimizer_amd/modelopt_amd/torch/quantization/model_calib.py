@@ -346,9 +346,10 @@ def _mse_fast(out, ref) -> bool:
 
 
 # Fused AWQ search on MFMA (csrc/mtq_awq_gemm.hip): used for linears with at most this many output
-# features, where it beats the per-alpha hipBLASLt path (k/v_proj: 1.4-1.6x, scripts/bench_awq_gemm.py);
-# wider linears keep hipBLASLt for the GEMM (its 1.5 PFLOP/s vs the fused kernel's ~1.0).
-# MTQ_AMD_AWQ_FUSED: "auto" (default), "always", "never".
+# features, where it beats the library path (k/v_proj, scripts/bench_awq_gemm.py); wider linears run
+# one hipBLASLt GEMM per alpha between one x * (1/s) pass and one loss pass for all alphas.
+# MTQ_AMD_AWQ_FUSED: "auto" (default), "always" (fused kernel for every width), "library" (the
+# hipBLASLt path for every width), "never" (the reference's per-alpha loop, no fast path).
 _AWQ_FUSED_MAX_N = 2048
 _AWQ_FUSED_MAX_G = 64
 _AWQ_FUSED = os.environ.get("MTQ_AMD_AWQ_FUSED", "auto")
@@ -406,15 +407,18 @@ def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
     # batched path's loss pass takes G <= 16; anything else runs one alpha at a time
     fused_ok = n_alpha <= _AWQ_FUSED_MAX_G and x2.shape[0] * k_in < 2**31 and n_out * k_in < 2**31
     fused = fused_ok and (_AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and n_out <= _AWQ_FUSED_MAX_N))
+    if _AWQ_FUSED not in ("auto", "always", "library"):
+        raise ValueError(f"MTQ_AMD_AWQ_FUSED={_AWQ_FUSED!r}: expected auto, always, library or never")
     if fused:
         ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
     elif n_alpha <= 16:
-        # wide linears: x * (1/s) for every alpha in one pass, the alphas' GEMMs as one batched
-        # hipBLASLt call (bias in its fp32 epilogue, one rounding, as F.linear), all losses in
-        # one pass that reads out_actual once
-        # (per-alpha torch.mm into slices of one [G, M, N] output, the GEMM F.linear itself uses:
-        # torch.bmm with the transposed [G, K, N] weight view faulted the GPU in hipBLASLt on
-        # ROCm 7 at [11, 8192, 4096] x [11, 4096, 4096])
+        # wide linears: x * (1/s) for every alpha in one pass, one hipBLASLt GEMM per alpha into
+        # slices of one [G, M, N] output (bias in its fp32 epilogue, one rounding, as F.linear;
+        # per-alpha torch.mm, the GEMM F.linear itself uses: torch.bmm with the transposed
+        # [G, K, N] weight view faulted the GPU in hipBLASLt on ROCm 7 at [11, 8192, 4096] x
+        # [11, 4096, 4096]), all losses in one pass that reads out_actual once.  Serial on one
+        # stream: the prescale and loss passes on a side stream beside the GEMMs were measured
+        # 5-30 % slower (they displace GEMM workgroups; profiles/r04/awq/overlap_ab_r04e.json).
         try:
             xs = ops.awq_prescale(x2, sinv)
             out = torch.empty((xs.shape[0], xs.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)

@@ -65,7 +65,7 @@ def _run(gpu, mode, alpha_step=0.1):
     return model, t
 
 
-@pytest.mark.parametrize("mode", ["auto", "always", "never"])
+@pytest.mark.parametrize("mode", ["auto", "always", "library", "never"])
 def test_awq_lite_int4_b128_matches_reference(gpu, mode):
     model, t = _run(gpu, mode)
     meta = json.loads((G / "awq_b128.json").read_text())

@@ -135,7 +135,7 @@ def _awq_run(gpu, mode):
     return m
 
 
-@pytest.mark.parametrize("mode", ["always", "auto"])
+@pytest.mark.parametrize("mode", ["always", "auto", "library"])
 def test_awq_lite_fused_search_matches_per_alpha_path(gpu, mode):
     """awq_lite end to end with the fused MFMA search ("always"; "auto" sends the 2048-wide
     linear and narrower ones to it and the rest to batched hipBLASLt + the multi-alpha loss pass)
@@ -168,3 +168,4 @@ def test_prescale_and_mse_multi(gpu, G):
     again = torch.zeros(G, device=gpu)
     _ext.ops().awq_mse_multi(out, ref, again)
     assert torch.equal(loss, again)
+
