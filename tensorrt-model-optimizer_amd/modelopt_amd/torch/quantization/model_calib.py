@@ -258,6 +258,21 @@ def get_act_scale(x):
     return x.abs().contiguous().view(-1, x.shape[-1]).mean(0).to(torch.float32)
 
 
+# The linears that read one tensor (q/k/v_proj, gate/up_proj) each take its act scale in the caching
+# pass; the last result is kept for the same tensor object at the same version (the reference
+# recomputes it per linear: same ops, same value).
+_act_scale_memo = [None, None, None]  # weakref to the tensor, its _version, the act scale
+
+
+def _act_scale_shared(x):
+    ref, ver, val = _act_scale_memo
+    if ref is not None and ref() is x and ver == x._version:
+        return val
+    val = get_act_scale(x)
+    _act_scale_memo[:] = [weakref.ref(x), x._version, val]
+    return val
+
+
 def get_scale(x_max, w_max, alpha, tensor_parallel_group=None):
     """AWQ scale for one alpha (reference :1474-1487)."""
     scales = (
@@ -457,7 +472,7 @@ def _awq_forward(self, input, *args, **kwargs):
         return out_actual
 
     if _AWQLiteHelper.cache_mode:
-        helper.act_scale = helper.act_scale + get_act_scale(self.input_quantizer(input))
+        helper.act_scale = helper.act_scale + _act_scale_shared(self.input_quantizer(input))
         helper.num_cache_steps += 1
         helper.num_tokens += input.numel() / input.shape[-1]
         if helper.is_input_quantized:
