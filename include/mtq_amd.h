@@ -125,6 +125,29 @@ float mtq_convert_to_exmy(float x, int format);
 int mtq_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtype, float *out,
                     hipStream_t stream);
 
+/* Calibration bookkeeping on the running-max buffers, in this library so that a calibration
+ * pass launches no kernel the model's own forward has not already loaded (the first launch of a
+ * kernel from another code object stalls the host for tens to hundreds of ms on the GPU box,
+ * DESIGN §4 "First-use stalls"):
+ *  mtq_amax_fill:  out[i] = value for i < n (0 starts a running max).
+ *  mtq_amax_fold:  dst[i] = max(dst[i], src[i]) for fp32 running maxima of |x| (NaN propagates,
+ *                  as torch.maximum); the shared-collect fold of MaxCalibrator (calib/max.py).
+ *  mtq_amax_check: flags[0] = any NaN, flags[1] = any +-inf, flags[2] = any value < 0 over the
+ *                  n elements of x (fp32 / bf16 / f16), written by one workgroup (no prior
+ *                  zeroing): the reference's per-collect asserts (calib/max.py:69-77) and
+ *                  validate_attr checks (tensor_quantizer.py:757-773) batched over many
+ *                  quantizers; flags is int32[3] device memory. */
+int mtq_amax_fill(float *out, int64_t n, float value, hipStream_t stream);
+int mtq_amax_fold(float *dst, const float *src, int64_t n, hipStream_t stream);
+int mtq_amax_check(const void *x, int64_t n, int dtype, int32_t *flags, hipStream_t stream);
+
+/* MoE shared input quantizer (huggingface.py _QuantFusedExperts, the once-per-layer form of the
+ * reference's per-expert input quantizer calls, plugins/huggingface.py:976-1115): y[r, :] = x[r, :]
+ * when any of row r's k expert indices (idx int64 [rows, k]) lies in [0, num_experts), else +0
+ * (rows routed to no local expert, e.g. expert-parallel sentinels).  x, y [rows, cols] of dtype. */
+int mtq_mask_unrouted_rows(const void *x, void *y, const int64_t *idx, int64_t rows, int64_t cols, int k,
+                           int64_t num_experts, int dtype, hipStream_t stream);
+
 /* Fused dynamic INT-n block quant with in-kernel block amax and an optional per-column
  * pre-quant scale:  t = T(x * pqs[col]) (rounded to the input dtype, as the reference's
  * `inputs * pre_quant_scale`, tensor_quantizer.py:1143-1144), per block of `block` along

@@ -829,6 +829,78 @@ int launch_amax_persist(const T *x, int64_t n, int64_t nvec, uint32_t *out, int 
   return check_launch();
 }
 
+// Calibration bookkeeping (mtq_amax_fill / _fold / _check): tiny launches that live in this code
+// object so the calibration pass needs no kernel the model's forward has not loaded.
+__global__ __launch_bounds__(kThreads) void amax_fill_kernel(float *__restrict__ out, int64_t n, float value) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) out[i] = value;
+}
+
+// dst = max(dst, src) with a NaN of either operand propagating, as torch.maximum (which NaN is
+// kept when both are NaN is not part of the contract)
+__global__ __launch_bounds__(kThreads) void amax_fold_kernel(float *__restrict__ dst, const float *__restrict__ src,
+                                                             int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const float a = dst[i], b = src[i];
+    dst[i] = (a != a) ? a : (b != b) ? b : fmaxf(a, b);
+  }
+}
+
+// one workgroup: grid-stride flags, wave OR, LDS OR, thread 0 writes all three
+constexpr int kCheckThreads = 1024;
+template <typename T>
+__global__ __launch_bounds__(kCheckThreads) void amax_check_kernel(const T *__restrict__ x, int64_t n,
+                                                                  int32_t *__restrict__ flags) {
+  int nan = 0, inf = 0, neg = 0;
+  for (int64_t i = threadIdx.x; i < n; i += kCheckThreads) {
+    const float v = Elem<T>::ld(x[i]);
+    nan |= v != v;
+    inf |= fabsf(v) == __builtin_inff();
+    neg |= v < 0.f;
+  }
+  int bits = nan | (inf << 1) | (neg << 2);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) bits |= __shfl_xor(bits, o);
+  __shared__ int red[kCheckThreads / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kCheckThreads / 64; ++w) bits |= red[w];
+    flags[0] = bits & 1;
+    flags[1] = (bits >> 1) & 1;
+    flags[2] = (bits >> 2) & 1;
+  }
+}
+
+// y[r, :] = x[r, :] if any of row r's k expert indices lies in [0, E), else +0 (the MoE shared
+// input quantizer's masking of rows routed to no local expert, huggingface.py _QuantFusedExperts):
+// one pass instead of the compare / and / any / where sequence.  VEC: 16-byte vectors (cols a
+// multiple of the vector, 16-byte aligned), else one element per lane.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kThreads) void mask_rows_kernel(const T *__restrict__ x, T *__restrict__ y,
+                                                             const int64_t *__restrict__ idx, int64_t rows,
+                                                             int64_t cols, int k, int64_t experts) {
+  constexpr int N = VEC ? Vec<T>::N : 1;
+  const int64_t per_row = cols / N, total = rows * per_row;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total; i += stride) {
+    const int64_t r = i / per_row;
+    bool routed = false;
+    for (int j = 0; j < k; ++j) {
+      const int64_t e = idx[r * k + j];
+      routed |= (e >= 0) & (e < experts);
+    }
+    if constexpr (VEC) {
+      Vec<T> v = ldg_vec(x + i * N);
+      if (!routed) v.raw = make_uint4(0u, 0u, 0u, 0u);
+      stg_vec(y + i * N, v);
+    } else {
+      y[i] = routed ? x[i] : Elem<T>::st(0.f);
+    }
+  }
+}
+
 // Generic: one element per lane, atomicMax per element (any P, K, Q, alignment).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void amax_generic_kernel(const T *__restrict__ x,
@@ -2561,6 +2633,49 @@ int mtq_reduce_amax(const void *x, int64_t P, int64_t K, int64_t Q, int dtype, f
   return dispatch_dtype_nof64(dtype, [&](auto t) {
     using T = decltype(t);
     return launch_amax<T>(x, P, K, Q, out, stream);
+  });
+}
+
+int mtq_amax_fill(float *out, int64_t n, float value, hipStream_t stream) {
+  if (n < 0 || (n > 0 && !out)) return MTQ_ERR_INVALID_ARG;
+  if (n == 0) return MTQ_OK;
+  amax_fill_kernel<<<grid_for(n, kThreads), kThreads, 0, stream>>>(out, n, value);
+  return check_launch();
+}
+
+int mtq_amax_fold(float *dst, const float *src, int64_t n, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!dst || !src))) return MTQ_ERR_INVALID_ARG;
+  if (n == 0) return MTQ_OK;
+  amax_fold_kernel<<<grid_for(n, kThreads), kThreads, 0, stream>>>(dst, src, n);
+  return check_launch();
+}
+
+int mtq_amax_check(const void *x, int64_t n, int dtype, int32_t *flags, hipStream_t stream) {
+  if (n < 0 || !flags || (n > 0 && !x)) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    amax_check_kernel<T><<<1, kCheckThreads, 0, stream>>>(reinterpret_cast<const T *>(x), n, flags);
+    return check_launch();
+  });
+}
+
+int mtq_mask_unrouted_rows(const void *x, void *y, const int64_t *idx, int64_t rows, int64_t cols, int k,
+                           int64_t num_experts, int dtype, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || k < 1 || num_experts < 1) return MTQ_ERR_INVALID_ARG;
+  if (rows == 0 || cols == 0) return MTQ_OK;
+  if (!x || !y || !idx) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    const T *xt = reinterpret_cast<const T *>(x);
+    T *yt = reinterpret_cast<T *>(y);
+    if (cols % N == 0 && aligned16(x) && aligned16(y))
+      mask_rows_kernel<T, true><<<grid_for(rows * cols / N, kThreads), kThreads, 0, stream>>>(xt, yt, idx, rows, cols, k,
+                                                                                          num_experts);
+    else
+      mask_rows_kernel<T, false><<<grid_for(rows * cols, kThreads), kThreads, 0, stream>>>(xt, yt, idx, rows, cols, k,
+                                                                                       num_experts);
+    return check_launch();
   });
 }
 

@@ -379,6 +379,56 @@ void amax_accumulate(const at::Tensor &inputs, at::Tensor out, int64_t P, int64_
   check_status(st, "reduce_amax");
 }
 
+// Calibration bookkeeping on fp32 running-max buffers (mtq_amax_fill / _fold / _check): kept in
+// the kernel library so a calibration pass loads no code object the model's forward has not.
+void amax_fill_(at::Tensor out, double value) {
+  check_device(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous(), "amax_fill_: contiguous fp32 tensor");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(out.device());
+  check_status(mtq_amax_fill(out.data_ptr<float>(), out.numel(), (float)value, cur_stream(out)), "amax_fill_");
+}
+
+void amax_fold_(at::Tensor dst, const at::Tensor &src) {
+  check_device(dst, "dst");
+  check_device(src, "src");
+  TORCH_CHECK(dst.scalar_type() == at::kFloat && src.scalar_type() == at::kFloat && dst.is_contiguous() &&
+                  src.is_contiguous() && dst.numel() == src.numel() && dst.device() == src.device(),
+              "amax_fold_: contiguous fp32 tensors of equal size on one device");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dst.device());
+  check_status(mtq_amax_fold(dst.data_ptr<float>(), src.data_ptr<float>(), dst.numel(), cur_stream(dst)),
+               "amax_fold_");
+}
+
+// int32 [3] on x's device: any NaN, any +-inf, any negative value
+at::Tensor amax_check(const at::Tensor &x) {
+  check_device(x, "x");
+  at::Tensor xc = x.contiguous();
+  const int dt = checked_dtype(xc, "x");
+  TORCH_CHECK(dt != MTQ_F64, "amax_check: float64 is not supported");
+  at::Tensor flags = at::empty({3}, xc.options().dtype(at::kInt));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(xc.device());
+  check_status(mtq_amax_check(xc.data_ptr(), xc.numel(), dt, flags.data_ptr<int32_t>(), cur_stream(xc)),
+               "amax_check");
+  return flags;
+}
+
+// hidden_states with the rows routed to no local expert zeroed (mtq_mask_unrouted_rows)
+at::Tensor mask_unrouted_rows(const at::Tensor &x, const at::Tensor &idx, int64_t num_experts) {
+  check_device(x, "hidden_states");
+  check_device(idx, "top_k_index");
+  TORCH_CHECK(x.dim() == 2 && idx.dim() == 2 && idx.size(0) == x.size(0) && idx.size(1) >= 1 &&
+                  idx.scalar_type() == at::kLong && idx.device() == x.device(),
+              "mask_unrouted_rows: hidden_states [T, H] and int64 top_k_index [T, k] on one device");
+  at::Tensor xc = x.contiguous(), ic = idx.contiguous();
+  at::Tensor y = at::empty_like(xc);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(xc.device());
+  check_status(mtq_mask_unrouted_rows(xc.data_ptr(), y.data_ptr(), ic.data_ptr<int64_t>(), xc.size(0), xc.size(1),
+                                      (int)ic.size(1), num_experts, checked_dtype(xc, "hidden_states"),
+                                      cur_stream(xc)),
+               "mask_unrouted_rows");
+  return y;
+}
+
 // Persistent zero-initialised workspace per (device, stream) for the deterministic MSE
 // reduction; the kernel restores its counter, so the buffer is filled once.
 at::Tensor mse_workspace(const at::Tensor &like, int64_t floats) {
@@ -1023,6 +1073,10 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("fused_amax_convert(Tensor inputs, int block_size, int format, int scale_format, "
         "Tensor? global_amax=None) -> Tensor");
   m.def("amax_accumulate(Tensor inputs, Tensor(a!) out, int P, int K, int Q) -> ()");
+  m.def("amax_fill_(Tensor(a!) out, float value) -> ()");
+  m.def("amax_fold_(Tensor(a!) dst, Tensor src) -> ()");
+  m.def("amax_check(Tensor x) -> Tensor");
+  m.def("mask_unrouted_rows(Tensor hidden_states, Tensor top_k_index, int num_experts) -> Tensor");
   m.def("block_quant_dynamic(Tensor inputs, Tensor? pre_quant_scale, int block, int num_bits, "
         "bool unsigned, bool narrow_range) -> Tensor");
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
@@ -1070,6 +1124,10 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("fake_e4m3fy_with_axis", &fake_e4m3fy_with_axis);
   m.impl("e4m3_cast", &e4m3_cast);
   m.impl("fused_amax_convert", &fused_amax_convert);
+  m.impl("amax_fill_", &amax_fill_);
+  m.impl("amax_fold_", &amax_fold_);
+  m.impl("amax_check", &amax_check);
+  m.impl("mask_unrouted_rows", &mask_unrouted_rows);
   m.impl("amax_accumulate", &amax_accumulate);
   m.impl("block_quant_dynamic", &block_quant_dynamic);
   m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);

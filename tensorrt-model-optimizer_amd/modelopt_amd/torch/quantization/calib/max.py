@@ -35,6 +35,38 @@ _SHARED = None
 _EPOCH = 0
 
 
+def _ops():
+    from modelopt_amd._ext import ops
+
+    return ops()
+
+
+def _zeros_f32(numel: int, device) -> torch.Tensor:
+    """A zeroed fp32 running-max buffer.  On the GPU the fill is the kernel library's own, so a
+    calibration pass launches no torch kernel the model's forward has not loaded (the first launch
+    from a code object not loaded yet stalls the host for tens to hundreds of ms)."""
+    if torch.device(device).type != "cuda":
+        return torch.zeros(numel, dtype=torch.float32, device=device)
+    t = torch.empty(numel, dtype=torch.float32, device=device)
+    _ops().amax_fill_(t, 0.0)
+    return t
+
+
+def _fold_max(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """dst = max(dst, src) (NaN propagates), the library's kernel on the GPU (see _zeros_f32)."""
+    if dst.is_cuda:
+        _ops().amax_fold_(dst, src)
+    else:
+        torch.maximum(dst, src, out=dst)
+
+
+def _bad_flags(x: torch.Tensor) -> torch.Tensor:
+    """int32 [3] on x's device: any NaN, any +-inf, any negative value (one launch on the GPU)."""
+    if x.is_cuda:
+        return _ops().amax_check(x)
+    return torch.stack([torch.isnan(x).any(), torch.isinf(x).any(), (x < 0).any()]).to(torch.int32)
+
+
 def new_collect_epoch() -> None:
     """Forget every calibrator's "same tensor as last collect" key (``.data`` writes between
     calibration passes do not bump ``_version``, so a key may not outlive its pass)."""
@@ -114,7 +146,7 @@ class MaxCalibrator(_Calibrator):
             numel = 1
             for s in keep_shape:
                 numel *= s
-            self._acc = torch.zeros(numel, dtype=torch.float32, device=x.device)
+            self._acc = _zeros_f32(numel, x.device)
             self._out_shape = keep_shape
             self._out_dtype = x.dtype if x.dtype.is_floating_point else torch.float32
             if self._out_dtype in (torch.float8_e4m3fn, torch.float8_e5m2):
@@ -151,7 +183,7 @@ class MaxCalibrator(_Calibrator):
         if entry is not None and entry[0]() is base and entry[1] == key and entry[2]() is not self:
             result = entry[3]
             if result is not None and result.numel() == self._acc.numel():
-                torch.maximum(self._acc, result, out=self._acc)
+                _fold_max(self._acc, result)
                 return
             producer = entry[2]()
             if producer is not None:
@@ -161,9 +193,12 @@ class MaxCalibrator(_Calibrator):
         if getattr(self, "_share", False):
             if self._tmp is None or self._tmp.numel() != self._acc.numel():
                 self._tmp = torch.empty_like(self._acc)
-            self._tmp.zero_()
+            if self._tmp.is_cuda:
+                _ops().amax_fill_(self._tmp, 0.0)
+            else:
+                self._tmp.zero_()
             quant_utils.reduce_amax_accumulate(x, self._tmp, reduce_axis)
-            torch.maximum(self._acc, self._tmp, out=self._acc)
+            _fold_max(self._acc, self._tmp)
             _SHARED = (weakref.ref(base), key, weakref.ref(self), self._tmp)
         else:
             quant_utils.reduce_amax_accumulate(x, self._acc, reduce_axis)
@@ -196,7 +231,7 @@ class MaxCalibrator(_Calibrator):
         """The reference's per-collect asserts (calib/max.py:69-77), evaluated once."""
         if self._acc is None or self._validated:
             return
-        bad = torch.stack([torch.isnan(self._acc).any(), torch.isinf(self._acc).any()]).tolist()
+        bad = _bad_flags(self._acc).tolist()
         assert not bad[0], "detected nan values in amax (NaN in a collected tensor)"
         assert not bad[1], "detected inf values in amax (inf in a collected tensor)"
         self._validated = True
@@ -212,8 +247,8 @@ class MaxCalibrator(_Calibrator):
             if isinstance(c, MaxCalibrator) and c._acc is not None and not c._validated:
                 by_dev.setdefault(c._acc.device, []).append(c)
         for cs in by_dev.values():
-            flat = torch.cat([c._acc for c in cs])
-            if not bool((~torch.isfinite(flat)).any()):
+            flags = _bad_flags(torch.cat([c._acc for c in cs])).tolist()
+            if not (flags[0] or flags[1]):
                 for c in cs:
                     c._validated = True
 

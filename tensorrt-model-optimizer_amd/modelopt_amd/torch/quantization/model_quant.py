@@ -89,6 +89,8 @@ def _validate_quantizer_attrs(model: nn.Module) -> None:
     as one batched check per device -- each per-quantizer check is three host syncs, ~1.3 k for
     Llama-3-8B.  Only when the batch holds a negative / inf / NaN value are the quantizers
     checked one by one, which emits the reference's per-quantizer warnings."""
+    from .calib.max import _bad_flags
+
     found = []
     for name, module in model.named_modules():
         if isinstance(module, TensorQuantizer):
@@ -100,13 +102,17 @@ def _validate_quantizer_attrs(model: nn.Module) -> None:
     for item in found:
         groups.setdefault((item[3].device, item[3].dtype), []).append(item)
     by_dev: dict = {}
-    for (dev, _), items in groups.items():
+    for (dev, dt), items in groups.items():
         flat = torch.cat([v.detach().reshape(-1) for *_, v in items])
-        by_dev.setdefault(dev, []).append((((flat < 0) | ~torch.isfinite(flat)).any(), items))
+        if dt in (torch.float32, torch.bfloat16, torch.float16):
+            flags = _bad_flags(flat)  # NaN, inf, negative: the library's kernel on the GPU
+        else:
+            flags = torch.stack([((flat < 0) | ~torch.isfinite(flat)).any()] * 3).to(torch.int32)
+        by_dev.setdefault(dev, []).append((flags, items))
     for checks in by_dev.values():
-        bad = torch.stack([c for c, _ in checks]).tolist()  # one host sync per device
-        for flag, (_, items) in zip(bad, checks):
-            if flag:
+        bad = torch.cat([c for c, _ in checks]).tolist()  # one host sync per device
+        for i, (_, items) in enumerate(checks):
+            if any(bad[3 * i : 3 * i + 3]):
                 for name, module, attr_name, _ in items:
                     module.validate_attr(attr_name=attr_name, warn_error=True, name=name)
 

@@ -86,8 +86,14 @@ class _QuantFusedExperts(QuantModule):
             isinstance(hs, torch.Tensor) and hs.dim() == 2 and isinstance(idx_t, torch.Tensor)
             and idx_t.dim() == 2 and idx_t.shape[0] == hs.shape[0] and _token_separable(first_in)
         ):
-            routed = ((idx_t >= 0) & (idx_t < self.num_experts)).any(dim=-1, keepdim=True)
-            hs = first_in(torch.where(routed, hs, hs.new_zeros(())))
+            if hs.is_cuda and idx_t.dtype == torch.int64 and idx_t.device == hs.device:
+                # one library pass (no compare / any / where kernels to load on first use)
+                from modelopt_amd._ext import ops as _ops
+
+                hs = first_in(_ops().mask_unrouted_rows(hs, idx_t, self.num_experts))
+            else:
+                routed = ((idx_t >= 0) & (idx_t < self.num_experts)).any(dim=-1, keepdim=True)
+                hs = first_in(torch.where(routed, hs, hs.new_zeros(())))
             if args:
                 args[0] = hs
             else:
