@@ -134,8 +134,8 @@ class MaxCalibrator(_Calibrator):
         return self._collect(x)
 
     def _collect(self, x):
-        reduce_axis = quant_utils.convert_quantization_axis_to_reduce_axis(x, self._axis)
-        if x.device.type == "meta":
+        reduce_axis = None if self._axis is None else quant_utils.convert_quantization_axis_to_reduce_axis(x, self._axis)
+        if x.is_meta:
             self._meta_amax = quant_utils.amax_view(x, reduce_axis)[4]
             return
         vk = None if x.is_inference() else self._view_key(x)

@@ -763,6 +763,19 @@ class TensorQuantizer(nn.Module):
     # ---- forward --------------------------------------------------------------------------------
     def forward(self, inputs):
         """Quantize/calibrate ``inputs`` (reference :1119-1221)."""
+        d = self.__dict__
+        if (
+            type(inputs) is torch.Tensor and d["_if_calib"] and not d["_if_quant"] and not d["_disabled"]
+            and not d["_dynamic"] and d.get("_block_sizes") is None and self.pre_quant_scale is None
+        ):
+            # collect-only (max / histogram calibration, no fake quant): the common calibration
+            # call, on the host's critical path in loops that sync per call (the eager MoE expert
+            # loop); the same steps as below with the inapplicable branches skipped
+            if inputs.numel() != 0:
+                if d["_calibrator"] is None:
+                    raise RuntimeError("Calibrator was not created.")
+                self.collect(inputs)
+            return inputs
         if isinstance(inputs, (BaseQuantizedTensor, QTensorWrapper)):  # a compressed weight
             assert self._dequantize, "No dequantization stats in the tensor quantizer."
             return self.dequantize(inputs)

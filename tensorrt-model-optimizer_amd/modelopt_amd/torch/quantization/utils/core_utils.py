@@ -106,6 +106,12 @@ def reduce_amax_accumulate(input: torch.Tensor, out: torch.Tensor, reduce_axis=N
     This is the running-max accumulator of ``MaxCalibrator.collect`` (calib/max.py:53-86) fused
     with ``reduce_amax``: no intermediate amax tensor, no host-side NaN/inf asserts.
     """
+    if reduce_axis is None and input.dtype in _KERNEL_DTYPES and input.is_contiguous():
+        # per-tensor max of a contiguous tensor (the common activation collect): no view mapping
+        n = input.numel()
+        if n:
+            _amax_op()(input, out if out.dim() == 1 else out.view(-1), 1, 1, n)
+        return
     if input.dtype in _FP8_DTYPES:
         input = input.to(torch.get_default_dtype())
     x, P, K, Q, _ = amax_view(input, reduce_axis)
@@ -114,7 +120,18 @@ def reduce_amax_accumulate(input: torch.Tensor, out: torch.Tensor, reduce_axis=N
     if x.dtype not in _KERNEL_DTYPES:
         # float64 has no HIP reduction kernel (fp32 accumulation would round it)
         raise TypeError(f"modelopt_amd: amax reduction does not support {x.dtype}")
-    _ext_ops().amax_accumulate(x, out.view(-1), P, K, Q)
+    _amax_op()(x, out.view(-1), P, K, Q)
+
+
+_AMAX_OP = []
+
+
+def _amax_op():
+    """The amax_accumulate OpOverload, resolved once (the packet lookup and overload resolution
+    of ``torch.ops.modelopt_amd.amax_accumulate`` cost microseconds on every collect)."""
+    if not _AMAX_OP:
+        _AMAX_OP.append(_ext_ops().amax_accumulate.default)
+    return _AMAX_OP[0]
 
 
 @torch.no_grad()
