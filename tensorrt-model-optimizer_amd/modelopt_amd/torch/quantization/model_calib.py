@@ -81,7 +81,13 @@ def finish_stats_collection(model: nn.Module, method: str | None = None, **kwarg
             continue
         cal = getattr(module, "_calibrator", None)
         if cal and not getattr(module, "_dynamic", False):
-            if method is not None:
+            if method is None and not kwargs and type(cal) is MaxCalibrator:
+                # load_calib_amax's steps with the amax computed once (its fp32 -> dtype cast is a
+                # fresh tensor: adopted without the setter's copy)
+                amax = cal.compute_amax()
+                if amax is not None:
+                    module._adopt_calib_amax(amax, cal)
+            elif method is not None:
                 if cal.compute_amax(method, **kwargs) is not None:
                     module.load_calib_amax(method, **kwargs)
             elif cal.compute_amax(**kwargs) is not None:

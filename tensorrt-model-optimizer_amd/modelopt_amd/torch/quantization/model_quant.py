@@ -3,8 +3,9 @@
 ``quantize(model, config, forward_loop)`` = convert (insert quantizers, apply the ordered
 wildcard ``quant_cfg``) + ``calibrate(model, config["algorithm"], forward_loop)``, as in
 model_quant.py:147-250.  The reference routes both through its mode framework (apply_mode /
-QuantizeModeDescriptor, mode.py); here they are direct calls with the same effects, and the
-quantizer state is recorded on ``model._modelopt_amd_state`` for save/restore.
+QuantizeModeDescriptor, mode.py); here they are direct calls with the same effects, the config is
+recorded on ``model._modelopt_amd_mode`` and ``mto.modelopt_state`` reads the quantizer state off
+the model when it is saved.
 """
 
 from __future__ import annotations
@@ -19,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .config import QuantizeConfig, algorithm_config
-from .conversion import quantizer_state, set_quantizer_attributes_partial
+from .conversion import set_quantizer_attributes_partial
 from .layerwise import layerwise_calibrate
 from .model_calib import awq, max_calibrate, mse_calibrate
 from .nn.modules.quant_module import QuantModule
@@ -137,7 +138,6 @@ def calibrate(model: nn.Module, algorithm="max", forward_loop: Callable | None =
     with _gc_paused():
         _validate_quantizer_attrs(model)
         model.train(is_training)
-        model.__dict__["_modelopt_amd_state"] = {"quantizer_state": quantizer_state(model)}
     return model
 
 

@@ -525,6 +525,18 @@ class TensorQuantizer(nn.Module):
                 )
         self.amax = calib_amax
 
+    def _adopt_calib_amax(self, amax: torch.Tensor, calibrator) -> None:
+        """``load_calib_amax`` for an amax the calibrator has just computed: the same checks, the
+        tensor kept as the buffer instead of copied, unless it aliases the calibrator's state."""
+        assert not self._dynamic, "Dynamic quantization does not need calibration."
+        acc = getattr(calibrator, "_acc", None)
+        if acc is not None and amax.untyped_storage().data_ptr() == acc.untyped_storage().data_ptr():
+            amax = amax.clone()
+        if "_amax" not in self._buffers:
+            self.register_buffer("_amax", amax.detach())
+        else:
+            self._amax_setter_helper(amax)
+
     def _get_amax(self, inputs):
         if self._use_constant_amax:
             return torch.tensor(torch.finfo(torch.float8_e4m3fn).max, device=inputs.device)
