@@ -3,7 +3,7 @@
 same 4 batches of 16 x 512 tokens profiled (torch.profiler, device time per kernel name) once
 without quantizers and once as mtq.quantize's forward_loop, printed as a diff sorted by the extra
 device time, plus host wall per batch of both (device synchronised per batch).
-    python scripts/prof_c2_diff.py [batches]"""
+    python scripts/prof_c2_diff.py [batches] [model] [config]   (e.g. 4 mixtral-8x7b FP8_DEFAULT_CFG)"""
 import json
 import sys
 import time
@@ -18,12 +18,17 @@ from torch.profiler import ProfilerActivity, profile  # noqa: E402
 from scripts import ptq_llama  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+model_name = sys.argv[2] if len(sys.argv) > 2 else "llama3-8b"
+config = sys.argv[3] if len(sys.argv) > 3 else "FP8_DEFAULT_CFG"
 import modelopt_amd.torch.quantization as mtq  # noqa: E402
 
 dev = torch.device("cuda")
-model = ptq_llama.build_model(32, dev, "llama3-8b")
+model = ptq_llama.build_model(32, dev, model_name)
+if model_name.startswith("mixtral"):
+    model.config._experts_implementation = "eager"
+vocab = ptq_llama.MODELS[model_name][1]["vocab_size"]
 g = torch.Generator(device=dev).manual_seed(1234)
-batches = list(torch.randint(0, 128256, (16 * nb, 512), device=dev, generator=g).split(16))
+batches = list(torch.randint(0, vocab, (16 * nb, 512), device=dev, generator=g).split(16))
 
 
 def kernel_table(prof):
@@ -58,7 +63,7 @@ def loop(m):
     prof["p1"] = p1
 
 
-mtq.quantize(model, mtq.FP8_DEFAULT_CFG, loop)
+mtq.quantize(model, getattr(mtq, config), loop)
 a, b = kernel_table(p0), kernel_table(prof["p1"])
 rows = []
 for k in set(a) | set(b):
