@@ -403,6 +403,7 @@ def _awq_search_tables(helper, dtype):
     if getattr(helper, "_tables", None) is None:
         s = _scale_table(helper.act_scale, helper.weight_scale, helper.alphas)
         helper._tables = ((1 / s).to(dtype), s.to(dtype))
+        helper._scale_rows = s  # fp32: the best alpha's row is the final scale (get_scale's bits)
     return helper._tables
 
 
@@ -740,7 +741,12 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
             # the reference's loss dict of floats (update_best_params, :1497-1511)
             h.loss = dict(zip(h.alphas, losses))
             h.best_alpha = min(h.loss, key=h.loss.get)
-            h.best_scale = get_scale(h.act_scale, h.weight_scale, h.best_alpha, None)
+            rows = getattr(h, "_scale_rows", None)
+            if rows is not None and rows.shape[0] == len(h.alphas):
+                h.best_scale = rows[h.alphas.index(h.best_alpha)].clone()  # == get_scale(best_alpha)
+            else:
+                h.best_scale = get_scale(h.act_scale, h.weight_scale, h.best_alpha, None)
+            h._scale_rows = None
         for q in (module.weight_quantizer, module.input_quantizer):
             if hasattr(q, "_pre_quant_scale"):
                 delattr(q, "_pre_quant_scale")
