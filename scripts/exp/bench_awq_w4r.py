@@ -20,7 +20,7 @@ ops = _ext.ops()
 lib = ctypes.CDLL(str(REPO / "scripts/exp/libawq_w4r.so"))
 lib.awq_w4r.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
-VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["1"])]
+VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "2"])]
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 SHAPES = {"k_proj": (1024, 4096), "q_proj": (4096, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
 M, G = 8192, 11

@@ -18,7 +18,7 @@ from modelopt_amd import _ext  # noqa: E402
 ops = _ext.ops()
 lib = ctypes.CDLL(str(REPO / "scripts/exp/libexport_exp.so"))
 lib.export_exp.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
-VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "1,2,3,4".split(","))]
+VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "5,6,7,8,9,10".split(","))]
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)

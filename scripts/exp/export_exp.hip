@@ -36,10 +36,95 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_pf_kernel(const T *__re
     for (int u = 0; u < U; ++u) v[u] = w[u];
   }
 }
+
+// One-shot product structure (U = 2 vectors per lane, all loads first) with the store kinds as
+// parameters: SNT = scale dword stores non-temporal, DNT = code stores non-temporal, LDS = the
+// workgroup's 128 scale bytes gathered in LDS and written by 32 lanes as one 128 B line instead of
+// 8 waves x 2 x 16 B non-temporal fragments.  bf16, block 32, native path (a lane whose block
+// leaves it falls back to the product function).
+template <bool SNT, bool DNT, bool LDS>
+__global__ __launch_bounds__(kThreads) void export_mxfp4_st_kernel(const __bf16 *__restrict__ x, uint8_t *__restrict__ y,
+                                                                   uint8_t *__restrict__ sc, int64_t nvec) {
+  using T = __bf16;
+  using V = Vec<T>;
+  constexpr int U = 2, LPB = 4;
+  __shared__ uint8_t sl[U * kThreads / LPB];
+  const int64_t wb = (int64_t)blockIdx.x * (kThreads * U);
+  const int64_t base = wb + threadIdx.x;
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * V::N);
+  }
+  const bool full = wb + kThreads * U <= nvec;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (!full) {
+      export_mxfp4_vec_one<T, 32, true>(i, v[u], y, sc, nvec, 1);
+      continue;
+    }
+    const uint32_t w[4] = {v[u].raw.x, v[u].raw.y, v[u].raw.z, v[u].raw.w};
+    const uint32_t m = group_max_u32<LPB>(scan_pairs(w).max_abs);
+    const float amax = half_bits_to_float<T>(m);
+    constexpr float kInv6 = 1.0f / 6.0f;
+    const float d6 = amax <= 3.402823466e38f ? div_rn(amax, 6.0f, kInv6) : amax * kInv6;
+    const float e = mx_e8m0_exponent(d6);
+    if (!(e >= -100.f && e <= 127.f)) {  // exact path, product function (writes its own scale)
+      export_mxfp4_vec_one<T, 32, true>(i, v[u], y, sc, nvec, 0);
+      if constexpr (LDS) {
+        if (threadIdx.x % LPB == 0) sl[u * (kThreads / LPB) + threadIdx.x / LPB] = (uint8_t)((uint32_t)(int)(e + 127.f) & 0xFFu);
+      }
+      continue;
+    }
+    const uint32_t sbyte = (uint32_t)(int)(e + 127.f) & 0xFFu;
+    if constexpr (LDS) {
+      if (threadIdx.x % LPB == 0) sl[u * (kThreads / LPB) + threadIdx.x / LPB] = (uint8_t)sbyte;
+    } else {
+      const uint32_t b1 = (uint32_t)__shfl_down((int)sbyte, 4, 16);
+      const uint32_t b2 = (uint32_t)__shfl_down((int)sbyte, 8, 16);
+      const uint32_t b3 = (uint32_t)__shfl_down((int)sbyte, 12, 16);
+      if ((threadIdx.x & 15) == 0) {
+        const uint32_t word = sbyte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(sc + i / LPB);
+        if constexpr (SNT) __builtin_nontemporal_store(word, dst);
+        else *dst = word;
+      }
+    }
+    const int ei = (int)e;
+    const float s = __uint_as_float((uint32_t)(ei + 127) << 23);
+    const float zthr = __uint_as_float(ei >= 24 ? (uint32_t)(ei - 23) << 23 : (ei >= 1 ? 1u << (ei - 1) : 0u));
+    uint32_t o = 0, zero = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float f0 = Elem<T>::ld(v[u].e[j]), f1 = Elem<T>::ld(v[u].e[j + 1]);
+      zero |= (fabsf(f0) <= zthr ? 0xFu : 0u) << (4 * j);
+      zero |= (fabsf(f1) <= zthr ? 0xFu : 0u) << (4 * j + 4);
+      o |= fp4_pair_hw(__uint_as_float(__float_as_uint(f0) - 1u), __uint_as_float(__float_as_uint(f1) - 1u), s) << (4 * j);
+    }
+    o = (o & ~zero) | (zero & 0x88888888u);
+    uint32_t *dy = reinterpret_cast<uint32_t *>(y + i * 4);
+    if constexpr (DNT) __builtin_nontemporal_store(o, dy);
+    else *dy = o;
+  }
+  if constexpr (LDS) {
+    if (full) {
+      __syncthreads();
+      if (threadIdx.x < U * kThreads / LPB / 4) {
+        const uint32_t word = reinterpret_cast<const uint32_t *>(sl)[threadIdx.x];
+        uint32_t *dst = reinterpret_cast<uint32_t *>(sc + wb / LPB) + threadIdx.x;
+        if constexpr (SNT) __builtin_nontemporal_store(word, dst);
+        else *dst = word;
+      }
+    }
+  }
+}
 }  // namespace
 
 // bf16 x [n], block 32, 4-byte aligned scales: var 1 = PF U=2 8 blocks/CU, 2 = PF U=2 4 blocks/CU,
-// 3 = PF U=1 8 blocks/CU, 4 = PF U=4 4 blocks/CU
+// 3 = PF U=1 8 blocks/CU, 4 = PF U=4 4 blocks/CU; 5..10 = one-shot store kinds (SNT, DNT, LDS):
+// 5 = (1,1,0) the product's, 6 = (0,1,0), 7 = (0,0,0), 8 = (1,1,1), 9 = (0,1,1), 10 = (0,0,1)
 extern "C" int export_exp(int var, const void *x, uint8_t *y, uint8_t *scales, int64_t n, hipStream_t stream) {
   if (n % 256 || ((uintptr_t)scales & 3) || ((uintptr_t)x & 15)) return 2;
   const int64_t nvec = n / 8;
@@ -50,6 +135,12 @@ extern "C" int export_exp(int var, const void *x, uint8_t *y, uint8_t *scales, i
   case 2: export_mxfp4_pf_kernel<2, __bf16, 32, true><<<cus * 4, kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   case 3: export_mxfp4_pf_kernel<1, __bf16, 32, true><<<cus * 8, kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   case 4: export_mxfp4_pf_kernel<4, __bf16, 32, true><<<cus * 4, kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 5: export_mxfp4_st_kernel<true, true, false><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 6: export_mxfp4_st_kernel<false, true, false><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 7: export_mxfp4_st_kernel<false, false, false><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 8: export_mxfp4_st_kernel<true, true, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 9: export_mxfp4_st_kernel<false, true, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 10: export_mxfp4_st_kernel<false, false, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   default: return 3;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
