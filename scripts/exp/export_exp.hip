@@ -42,12 +42,12 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_pf_kernel(const T *__re
 // workgroup's 128 scale bytes gathered in LDS and written by 32 lanes as one 128 B line instead of
 // 8 waves x 2 x 16 B non-temporal fragments.  bf16, block 32, native path (a lane whose block
 // leaves it falls back to the product function).
-template <bool SNT, bool DNT, bool LDS>
+template <bool SNT, bool DNT, bool LDS, int U = 2>
 __global__ __launch_bounds__(kThreads) void export_mxfp4_st_kernel(const __bf16 *__restrict__ x, uint8_t *__restrict__ y,
                                                                    uint8_t *__restrict__ sc, int64_t nvec) {
   using T = __bf16;
   using V = Vec<T>;
-  constexpr int U = 2, LPB = 4;
+  constexpr int LPB = 4;
   __shared__ uint8_t sl[U * kThreads / LPB];
   const int64_t wb = (int64_t)blockIdx.x * (kThreads * U);
   const int64_t base = wb + threadIdx.x;
@@ -124,7 +124,8 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_st_kernel(const __bf16 
 
 // bf16 x [n], block 32, 4-byte aligned scales: var 1 = PF U=2 8 blocks/CU, 2 = PF U=2 4 blocks/CU,
 // 3 = PF U=1 8 blocks/CU, 4 = PF U=4 4 blocks/CU; 5..10 = one-shot store kinds (SNT, DNT, LDS):
-// 5 = (1,1,0) the product's, 6 = (0,1,0), 7 = (0,0,0), 8 = (1,1,1), 9 = (0,1,1), 10 = (0,0,1)
+// 5 = (1,1,0) the product's, 6 = (0,1,0), 7 = (0,0,0), 8 = (1,1,1), 9 = (0,1,1), 10 = (0,0,1);
+// 11 / 12 / 13 = 8 with U = 4 / 8 / 1 vectors per lane
 extern "C" int export_exp(int var, const void *x, uint8_t *y, uint8_t *scales, int64_t n, hipStream_t stream) {
   if (n % 256 || ((uintptr_t)scales & 3) || ((uintptr_t)x & 15)) return 2;
   const int64_t nvec = n / 8;
@@ -141,6 +142,9 @@ extern "C" int export_exp(int var, const void *x, uint8_t *y, uint8_t *scales, i
   case 8: export_mxfp4_st_kernel<true, true, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   case 9: export_mxfp4_st_kernel<false, true, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   case 10: export_mxfp4_st_kernel<false, false, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 11: export_mxfp4_st_kernel<true, true, true, 4><<<export_grid(nvec, 4), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 12: export_mxfp4_st_kernel<true, true, true, 8><<<export_grid(nvec, 8), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 13: export_mxfp4_st_kernel<true, true, true, 1><<<export_grid(nvec, 1), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   default: return 3;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
