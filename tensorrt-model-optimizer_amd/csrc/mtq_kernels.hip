@@ -2213,13 +2213,15 @@ __device__ __forceinline__ void export_nvfp4_vec_one(int64_t i, const T *__restr
 }
 
 // MXFP4: LPB = block / N lanes per block, shuffle-max, every lane writes N/2 code bytes.  Scale
-// bytes: with 16-bit elements and block 32 (LPB 4) and a 4-byte aligned scale buffer (SC4), the
-// bytes of 4 consecutive blocks are gathered into lane 16 k of each 16-lane row and leave as one
-// dword store (4 stores per wave instead of 16 single-byte ones); otherwise the block's first lane
-// writes its byte.  The caller loads the lane's vector (all of a thread's loads issued first).
-template <typename T, int BLOCK, bool SC4>
+// bytes: with LDS, the block's first lane puts its byte into the workgroup's LDS line `sl` and the
+// kernel writes the line once (export_mxfp4_vec_kernel); with 16-bit elements and block 32 (LPB 4)
+// and a 4-byte aligned scale buffer (SC4), the bytes of 4 consecutive blocks are gathered into lane
+// 16 k of each 16-lane row and leave as one dword store; otherwise the block's first lane writes
+// its byte.  The caller loads the lane's vector (all of a thread's loads issued first).
+template <typename T, int BLOCK, bool SC4, bool LDS = false>
 __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y,
-                                                     uint8_t *__restrict__ sc, int64_t nvec, int native) {
+                                                     uint8_t *__restrict__ sc, int64_t nvec, int native,
+                                                     uint8_t *sl = nullptr) {
   using V = Vec<T>;
   constexpr int N = V::N;
   constexpr int LPB = BLOCK / N;
@@ -2256,7 +2258,9 @@ __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const Vec<T> &v,
   }
   const float e = mx_e8m0_exponent(d6);
   const uint32_t sbyte = (uint32_t)(int)(e + 127.f) & 0xFFu;
-  if constexpr (SC4) {
+  if constexpr (LDS) {
+    if (threadIdx.x % LPB == 0) sl[threadIdx.x / LPB] = (uint8_t)sbyte;
+  } else if constexpr (SC4) {
     static_assert(LPB == 4, "dword scale stores: 4 lanes per block");
     // lanes 16k .. 16k+15 hold blocks 4k' .. 4k'+3 (vector index i is lane-consecutive and the
     // chunk base a multiple of 256): gather the three neighbour blocks' bytes into lane 16k
@@ -2458,8 +2462,31 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
     const int64_t i = base + u * kThreads;
     v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * Vec<T>::N);
   }
+  if constexpr (SC4) {
+    // The workgroup's U * 64 scale bytes are consecutive: gathered in LDS and written as whole
+    // dwords by the first U * 16 lanes (one 128 B line for U = 2) instead of 8 waves x U
+    // non-temporal 16 B fragments, each a partial-line write (0.643 -> 0.689 of the roofline,
+    // profiles/r04/export/export_mxfp4_store_ab_r04v.json).
+    constexpr int NB = U * kThreads / LPB;
+    static_assert(NB % 4 == 0, "whole dwords of scale bytes");
+    __shared__ uint8_t sl[NB];
 #pragma unroll
-  for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK, SC4>(base + u * kThreads, v[u], y, sc, nvec, native);
+    for (int u = 0; u < U; ++u)
+      export_mxfp4_vec_one<T, BLOCK, true, true>(base + u * kThreads, v[u], y, sc, nvec, native,
+                                                 sl + u * (kThreads / LPB));
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * NB, nblk = nvec / LPB;
+    if (b0 + NB <= nblk) {
+      if (threadIdx.x < NB / 4)
+        __builtin_nontemporal_store(reinterpret_cast<const uint32_t *>(sl)[threadIdx.x],
+                                    reinterpret_cast<uint32_t *>(sc + b0) + threadIdx.x);
+    } else {
+      for (int t = threadIdx.x; t < NB && b0 + t < nblk; t += kThreads) sc[b0 + t] = sl[t];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) export_mxfp4_vec_one<T, BLOCK, false>(base + u * kThreads, v[u], y, sc, nvec, native);
+  }
 }
 
 // U = 2 consecutive 256-vector chunks per block (U = 1 / 4 within run-to-run noise,
