@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Measurement only: the AWQ search's per-alpha GEMMs (torch.mm of xs[g] [M, K] by wq[g]^T into a
 [G, M, N] slice, model_calib wide path) under PyTorch's default hipBLASLt heuristic against the
-solution TunableOp picks for the same shape, on Llama-3-8B shapes, 8192 tokens, 11 alphas.
-Writes the tuned-solution table to gpurun_out/tunableop_results.csv."""
+solution TunableOp picks for the same shape, on Llama-3-8B shapes, 8192 tokens, 11 alphas."""
 import json
 import os
 import statistics
@@ -70,5 +69,4 @@ for name, (N, K) in SHAPES.items():
     print(name, json.dumps(r), file=sys.stderr, flush=True)
     del xs, wq, out, ref
     torch.cuda.empty_cache()
-tun.write_file("gpurun_out/tunableop_results.csv")
 print(json.dumps(res))

@@ -149,3 +149,22 @@ extern "C" int export_exp(int var, const void *x, uint8_t *y, uint8_t *scales, i
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// FP8 per-tensor / NVFP4 export packers at U vectors per lane (the product's kernels, other U):
+// var 20 / 21 = export_fp8_pt_kernel U = 4 / 2 (round to dtype), 22 / 23 = export_nvfp4_vec_kernel
+// U = 4 / 2.  aux0 = the fp8 scale (1 float) or the NVFP4 block scales, aux1 = the NVFP4 scale_2.
+extern "C" int export_exp2(int var, const void *x, uint8_t *y, const float *aux0, const float *aux1, int64_t rows,
+                           int64_t cols, hipStream_t stream) {
+  const int64_t nvec = rows * cols / 8;
+  if (cols % 16 || ((uintptr_t)x & 15)) return 2;
+  const __bf16 *xt = reinterpret_cast<const __bf16 *>(x);
+  const FastDiv fvpb = make_fastdiv(2u);
+  switch (var) {
+  case 20: export_fp8_pt_kernel<4, __bf16, true><<<export_grid(nvec, 4), kThreads, 0, stream>>>(xt, y, nvec, aux0); break;
+  case 21: export_fp8_pt_kernel<2, __bf16, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, nvec, aux0); break;
+  case 22: export_nvfp4_vec_kernel<4, __bf16, true><<<export_grid(nvec, 4), kThreads, 0, stream>>>(xt, y, nvec, 2, fvpb, aux0, aux1, 1); break;
+  case 23: export_nvfp4_vec_kernel<2, __bf16, true><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, nvec, 2, fvpb, aux0, aux1, 1); break;
+  default: return 3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

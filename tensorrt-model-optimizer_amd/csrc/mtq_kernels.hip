@@ -2464,9 +2464,9 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_vec_kernel(const T *__r
   }
   if constexpr (SC4) {
     // The workgroup's U * 64 scale bytes are consecutive: gathered in LDS and written as whole
-    // dwords by the first U * 16 lanes (one 128 B line for U = 2) instead of 8 waves x U
-    // non-temporal 16 B fragments, each a partial-line write (0.643 -> 0.689 of the roofline,
-    // profiles/r04/export/export_mxfp4_store_ab_r04v.json).
+    // dwords by the first U * 16 lanes (two 128 B lines for U = 4) instead of 8 waves x U
+    // non-temporal 16 B fragments, each a partial-line write (0.643 -> 0.689 of the roofline at
+    // U = 2, profiles/r04/export/export_mxfp4_store_ab_r04v.json).
     constexpr int NB = U * kThreads / LPB;
     static_assert(NB % 4 == 0, "whole dwords of scale bytes");
     __shared__ uint8_t sl[NB];
@@ -3084,13 +3084,12 @@ int mtq_export_mxfp4(const void *x, uint8_t *y, uint8_t *scales, int64_t n, int 
     if (aligned16(x) && ((uintptr_t)y % (N / 2)) == 0 && (block == 32 || block == 16) && block % N == 0) {
       const int64_t nvec = n / N;
       const bool sc4 = N == 8 && block == 32 && ((uintptr_t)scales % 4) == 0;
-      if (block == 32 && sc4)
-        with_export_u([&](auto uc) {
-          constexpr int U = decltype(uc)::value;
-          if constexpr (N == 8)
-            export_mxfp4_vec_kernel<U, T, 32, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
-        });
-      else if (block == 32)
+      if (block == 32 && sc4) {
+        // U = 4 vectors per lane (256 scale bytes per workgroup): 0.69 -> 0.74 of the roofline
+        // against U = 2 (profiles/r04/export/export_mxfp4_store_ab_r04w.json)
+        if constexpr (N == 8)
+          export_mxfp4_vec_kernel<4, T, 32, true><<<export_grid(nvec, 4), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
+      } else if (block == 32)
         with_export_u([&](auto uc) {
           constexpr int U = decltype(uc)::value;
           export_mxfp4_vec_kernel<U, T, 32, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(reinterpret_cast<const T *>(x), y, scales, nvec, 1);
