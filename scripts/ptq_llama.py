@@ -17,6 +17,7 @@ C5 (``--model mixtral-8x7b``): Mixtral-8x7B dims (transformers-5 fused experts, 
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import sys
 import time
@@ -98,13 +99,19 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
 
     res = {"model": f"{label} dims, {layers} layers, bf16 random init", "samples": samples,
            "seq": seq, "batch": batch, "world": world, "config": config}
+    # Both timed regions start from a collected Python heap: building a 16-140 GB HF model leaves a
+    # generation-2 collection due (0.16 s on a 436 k-object heap, profiles/r04/ptq/c2_gc_r04zc.json)
+    # that otherwise fires inside whichever timed region allocates next -- the model build's debt,
+    # not quantization work.
     if baseline:
         forward_loop(model)  # warm-up (kernels, allocator)
+        gc.collect()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         forward_loop(model)
         torch.cuda.synchronize()
         res["bf16_forward_s"] = round(time.perf_counter() - t0, 3)
+    gc.collect()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     cfg = getattr(mtq, config)
