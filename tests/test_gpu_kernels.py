@@ -669,7 +669,9 @@ def test_export_nvfp4_vs_oracle(gpu, dtype, shape):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("shape", [(64, 256), (3, 96)])
+# (37, 4096) / (33, 8224): several 1024-vector workgroups and a partial last one (the packer's
+# LDS-gathered scale line falls back to byte stores there; 8481 blocks is not a multiple of 4)
+@pytest.mark.parametrize("shape", [(64, 256), (3, 96), (37, 4096), (33, 8224)])
 def test_export_mxfp4_vs_oracle(gpu, dtype, shape):
     g = torch.Generator().manual_seed(shape[1])
     w = (torch.randn(shape, generator=g) * torch.logspace(-3, 1, shape[1])).to(dtype)
