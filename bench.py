@@ -18,6 +18,8 @@ Also reported (same JSON line):
                 on this host's cores on a bounded sample (rank 0, N=1 only)
   ptq           Llama-3-8B FP8 PTQ wall-clock (512 synthetic samples x 512 tokens; DP over ranks,
                 slowest rank), the bf16 forward of the same batches at N=1, and the difference
+  ptq_c3        Llama-3-8B INT4 AWQ-lite (block 128) PTQ wall-clock, same calibration set
+  ptq_c5        Mixtral-8x7B FP8 PTQ wall-clock beside its bf16 forward (N=1 by default)
 
 Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one rank per GPU: under
 torch.distributed.run when RANK is set, otherwise bench.py starts that launcher itself as a child
@@ -238,7 +240,7 @@ def attention_suite(iters: int = 50):
     """The fused flash attention with softmax-P qdq (mtq_attention_fwd) on a Llama-3-8B
     calibration batch (16 x 512 tokens, 32 / 8 heads, D 128, bf16, causal): MFMA TFLOP/s per P
     mode vs the 2.5 PF dense bf16 peak, beside torch SDPA without P qdq."""
-    from scripts import bench_attention  # noqa: PLC0415
+    from benchmarks import attention as bench_attention  # noqa: PLC0415
 
     r = bench_attention.measure(iters=iters)
     peak = r["peak_tflops_bf16_dense"]
@@ -337,7 +339,7 @@ def cpu_e2e_baseline(samples: int = 8):
 
     from oracle import ref_ops as R  # test infrastructure: the CPU baseline only
 
-    from scripts.ptq_llama import LLAMA3_8B
+    from benchmarks.ptq_llama import LLAMA3_8B
 
     cfg = LlamaConfig(**LLAMA3_8B)
     cfg._attn_implementation = "sdpa"
@@ -403,8 +405,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-ptq", action="store_true", help="skip the Llama-3-8B FP8 PTQ wall-clock")
     ap.add_argument("--no-c3", action="store_true", help="skip the Llama-3-8B INT4 AWQ-lite PTQ (C3)")
-    ap.add_argument("--c5", action="store_true",
-                    help="also run C5: Mixtral-8x7B FP8 PTQ (93 GB bf16 resident, ~2 min) beside its bf16 forward")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip C5: Mixtral-8x7B FP8 PTQ (93 GB bf16 resident, ~40 s) beside its bf16 forward; it runs "
+                    "by default at N=1")
+    ap.add_argument("--c5", action="store_true", help="run C5 at N > 1 too (data-parallel, 93 GB per rank)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
                     help="cpu = plumbing rehearsal on the product's host kernels (default: cuda when a "
@@ -459,6 +463,7 @@ def main():
             "block": BLOCK,
             "parallelism": f"dp{world}",
             "sharding": "independent row shards per rank, no collective in the timed path",
+            "dist_backend": dist.get_backend() if dist is not None else None,
         },
         "roofline": {
             "bound": "hbm",
@@ -480,7 +485,7 @@ def main():
         out["kernels"] = kernel_suite(ops, xs, args.steps, args.warmup)
         out["attention_p_qdq"] = attention_suite()
     if not args.no_ptq:
-        from scripts import ptq_llama  # noqa: PLC0415
+        from benchmarks import ptq_llama  # noqa: PLC0415
 
         del xs, blk
         torch.cuda.empty_cache()
@@ -502,8 +507,8 @@ def main():
             r3["ptq_wall_clock_s"] = round(_max_over_ranks(dist, r3["ptq_wall_clock_s"]), 3)
             r3["calib_tokens_per_s"] = round(512 * 512 / r3["ptq_wall_clock_s"], 1)
             out["ptq_c3"] = r3
-        if args.c5:
-            # C5: Mixtral-8x7B FP8 PTQ over the MoE QuantLinear path (opt-in: builds a 93 GB model)
+        if not args.no_c5 and (world == 1 or args.c5):
+            # C5: Mixtral-8x7B FP8 PTQ over the MoE QuantLinear path (a 93 GB model per rank)
             print("bench: C5 Mixtral-8x7B FP8_DEFAULT_CFG PTQ ...", file=sys.stderr, flush=True)
             torch.cuda.empty_cache()
             _barrier(dist)

@@ -6,7 +6,7 @@ launches, against (a) torch SDPA (no P qdq: the unquantised floor) and (b) the e
 a P quantizer needs without a fused kernel (materialised scores, softmax, P fake quant, P @ V).
 MFMA FLOP per launch (causal, the reference kernel's work): 4 * B * Hq * D * sum_q (keys seen).
 
-Usage: python scripts/bench_attention.py [--iters 20] [--out file.json]
+Usage: python benchmarks/attention.py [--iters 20] [--out file.json]
 """
 
 from __future__ import annotations

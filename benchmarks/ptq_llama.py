@@ -11,7 +11,7 @@ quantizer overhead on top of the bf16 GEMMs is visible.
 C5 (``--model mixtral-8x7b``): Mixtral-8x7B dims (transformers-5 fused experts, 8 experts top-2,
 46.7 G params = 93 GB bf16, resident on one GPU), same calibration set (vocab 32000).
 
-    python scripts/ptq_llama.py [--model llama3-8b] [--layers 32] [--samples 512] [--seq 512] [--batch 16]
+    python benchmarks/ptq_llama.py [--model llama3-8b] [--layers 32] [--samples 512] [--seq 512] [--batch 16]
 """
 
 from __future__ import annotations
@@ -92,10 +92,28 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
     mine = ids[rank * per : (rank + 1) * per]
     batches = list(mine.split(batch))
 
+    passes = []  # (start, end) of every forward_loop call
+
     def forward_loop(m):
+        t = time.perf_counter()
         with torch.no_grad():
             for b in batches:
                 m(b)
+        torch.cuda.synchronize()
+        passes.append((t, time.perf_counter()))
+
+    gc_events = []
+
+    def _gc_cb(phase, info):  # cyclic-GC collections inside the timed regions (host time)
+        if phase == "start":
+            gc_events.append([info["generation"], time.perf_counter(), None])
+        elif gc_events and gc_events[-1][2] is None:
+            gc_events[-1][2] = time.perf_counter()
+
+    def gc_summary(t0, t1):
+        ev = [e for e in gc_events if e[2] is not None and t0 <= e[1] <= t1]
+        return {f"gen{g}": {"n": sum(1 for e in ev if e[0] == g),
+                            "s": round(sum(e[2] - e[1] for e in ev if e[0] == g), 4)} for g in (0, 1, 2)}
 
     res = {"model": f"{label} dims, {layers} layers, bf16 random init", "samples": samples,
            "seq": seq, "batch": batch, "world": world, "config": config}
@@ -107,10 +125,14 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
         forward_loop(model)  # warm-up (kernels, allocator)
         gc.collect()
         torch.cuda.synchronize()
+        gc.callbacks.append(_gc_cb)
         t0 = time.perf_counter()
         forward_loop(model)
         torch.cuda.synchronize()
-        res["bf16_forward_s"] = round(time.perf_counter() - t0, 3)
+        t1 = time.perf_counter()
+        gc.callbacks.remove(_gc_cb)
+        res["bf16_forward_s"] = round(t1 - t0, 3)
+        res["bf16_gc"] = gc_summary(t0, t1)
     gc.collect()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -125,9 +147,18 @@ def run(samples=512, seq=512, batch=16, layers=32, config="FP8_DEFAULT_CFG", ran
     if kv is not None:  # e.g. FP8_KV_CFG: K/V cache fake quant inside every attention
         cfg["quant_cfg"] = cfg["quant_cfg"] + getattr(mtq, kv)["quant_cfg"]
         res["kv"] = kv
+    gc.callbacks.append(_gc_cb)
+    passes.clear()
     mtq.quantize(model, cfg, forward_loop)
     torch.cuda.synchronize()
-    res["ptq_wall_clock_s"] = round(time.perf_counter() - t0, 3)
+    t1 = time.perf_counter()
+    gc.callbacks.remove(_gc_cb)
+    res["ptq_wall_clock_s"] = round(t1 - t0, 3)
+    if len(passes) == 1:  # one calibration pass (max): where the time outside the forward goes
+        (p0, p1), = passes
+        res["ptq_phases_s"] = {"before_first_batch": round(p0 - t0, 4), "calibration_forward": round(p1 - p0, 4),
+                               "after_last_batch": round(t1 - p1, 4)}
+    res["ptq_gc"] = gc_summary(t0, t1)
     n_q = sum(1 for _, m in model.named_modules() if isinstance(m, mtq.TensorQuantizer) and m.is_enabled)
     res["enabled_quantizers"] = n_q
     if baseline:

@@ -172,9 +172,11 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
 /* torch.histc's CPU accumulation for calls above 2^24 elements (calib/histogram.py:116-130 ->
  * torch.histc -> at::parallel_for): element chunk c is [bounds[c], bounds[c+1]) (device int64
  * [chunks + 1], e.g. the skip_zeros boundaries mapped back to the input), or, with bounds null,
- * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  Each chunk is counted exactly in one launch
- * into its row of `scratch` (uint32 [chunks, bins], zeroed here), then
- * hist[b] = sum_c min(fp32(scratch[c][b]), 2^24) in chunk order (overwritten, fp32 [bins]).
+ * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  One launch: each chunk is counted exactly
+ * into its row of `scratch` (uint32 [chunks * bins + 1]: the rows, then a block counter; ALL ZERO
+ * on entry, left all zero on return -- keep one per stream and reuse it), and the launch's last
+ * workgroup writes hist[b] = sum_c min(fp32(scratch[c][b]), 2^24) in chunk order (fp32 [bins],
+ * overwritten).
  * bf16 / f16 only, x 16-byte aligned, n % 8 == 0, bins <= 8192 (MTQ_ERR_DTYPE /
  * MTQ_ERR_INVALID_ARG otherwise: the caller counts chunk by chunk with mtq_histogram_abs). */
 int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,

@@ -9,7 +9,7 @@ MTQ_AMD_ATTN_STAGE=32 timeout -k 10 300 python -u -m pytest tests/test_gpu_atten
 tail -1 gpurun_out/${TAG}_tests32.log
 for r in 1 2; do
   for st in 64 32; do
-    MTQ_AMD_ATTN_STAGE=$st timeout -k 10 200 python -u scripts/bench_attention.py --iters 50 --out gpurun_out/${TAG}_s${st}_r$r.json > gpurun_out/${TAG}_s${st}_r$r.log 2>&1 || { tail -20 gpurun_out/${TAG}_s${st}_r$r.log; exit 11; }
+    MTQ_AMD_ATTN_STAGE=$st timeout -k 10 200 python -u benchmarks/attention.py --iters 50 --out gpurun_out/${TAG}_s${st}_r$r.json > gpurun_out/${TAG}_s${st}_r$r.log 2>&1 || { tail -20 gpurun_out/${TAG}_s${st}_r$r.log; exit 11; }
     python -c "import json;d=json.load(open('gpurun_out/${TAG}_s${st}_r$r.json'));print('stage $st round $r',{k:v['ms'] for k,v in d['modes'].items()})"
   done
 done

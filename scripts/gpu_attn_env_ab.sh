@@ -10,7 +10,7 @@ for v in "$@"; do
 done
 for r in 1 2; do
   for v in "$@"; do
-    env $VAR=$v timeout -k 10 200 python -u scripts/bench_attention.py --iters 50 --out gpurun_out/${TAG}_${v}_r$r.json > gpurun_out/${TAG}_${v}_r$r.log 2>&1 || { tail -20 gpurun_out/${TAG}_${v}_r$r.log; exit 11; }
+    env $VAR=$v timeout -k 10 200 python -u benchmarks/attention.py --iters 50 --out gpurun_out/${TAG}_${v}_r$r.json > gpurun_out/${TAG}_${v}_r$r.log 2>&1 || { tail -20 gpurun_out/${TAG}_${v}_r$r.log; exit 11; }
     python -c "import json;d=json.load(open('gpurun_out/${TAG}_${v}_r$r.json'));print('$VAR=$v round $r',{k:v['ms'] for k,v in d['modes'].items()})"
   done
 done

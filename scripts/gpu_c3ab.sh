@@ -8,6 +8,6 @@ TAG=${1:-c3ab}
 shift
 mkdir -p gpurun_out
 for m in "$@"; do
-  MTQ_AMD_AWQ_FUSED=$m timeout -k 10 300 python -u scripts/ptq_llama.py --config INT4_AWQ_CFG --no-baseline > gpurun_out/${TAG}_$m.json 2> gpurun_out/${TAG}_$m.err || { tail -20 gpurun_out/${TAG}_$m.err; exit 31; }
+  MTQ_AMD_AWQ_FUSED=$m timeout -k 10 300 python -u benchmarks/ptq_llama.py --config INT4_AWQ_CFG --no-baseline > gpurun_out/${TAG}_$m.json 2> gpurun_out/${TAG}_$m.err || { tail -20 gpurun_out/${TAG}_$m.err; exit 31; }
   echo "$m $(cat gpurun_out/${TAG}_$m.json)"
 done

@@ -8,7 +8,7 @@ shift
 mkdir -p gpurun_out
 for what in "$@"; do
   case $what in
-    c5) timeout -k 10 900 python -u scripts/ptq_llama.py --model mixtral-8x7b > gpurun_out/${TAG}_c5.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 21; }
+    c5) timeout -k 10 900 python -u benchmarks/ptq_llama.py --model mixtral-8x7b > gpurun_out/${TAG}_c5.json 2> gpurun_out/${TAG}_c5.err || { tail -20 gpurun_out/${TAG}_c5.err; exit 21; }
         cat gpurun_out/${TAG}_c5.json ;;
     c4) timeout -k 10 900 python -u scripts/ptq_sharded.py > gpurun_out/${TAG}_c4.json 2> gpurun_out/${TAG}_c4.err || { tail -20 gpurun_out/${TAG}_c4.err; exit 22; }
         cat gpurun_out/${TAG}_c4.json ;;

@@ -13,7 +13,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO / "tensorrt-model-optimizer_amd"), str(REPO)]
 import torch  # noqa: E402
 
-from scripts import ptq_llama  # noqa: E402
+from benchmarks import ptq_llama  # noqa: E402
 
 layers = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 samples = int(sys.argv[2]) if len(sys.argv) > 2 else 512

@@ -4,6 +4,7 @@ times of the bf16 forward (second pass, after a warm-up) and of the calibration 
 mtq.quantize, plus the quantize time before the first batch (conversion, weight amax pass) and after
 the last one (amax load, checks).  Shows which part of the PTQ-over-bf16 gap is per batch and which
 is one-time.  python scripts/prof_c5_batches.py [layers] [samples]"""
+import gc
 import json
 import sys
 import time
@@ -13,7 +14,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO / "tensorrt-model-optimizer_amd"), str(REPO)]
 import torch  # noqa: E402
 
-from scripts import ptq_llama  # noqa: E402
+from benchmarks import ptq_llama  # noqa: E402
 
 layers = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 samples = int(sys.argv[2]) if len(sys.argv) > 2 else 512
@@ -38,6 +39,7 @@ def loop(m, rec=None):
 
 
 loop(model)
+gc.collect()  # as benchmarks/ptq_llama.py: the model build's pending collection outside the timing
 torch.cuda.synchronize()
 bf = [time.perf_counter()]
 loop(model, bf)
@@ -51,6 +53,7 @@ def calib_loop(m):
     loop(m, marks)
 
 
+gc.collect()
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 mtq.quantize(model, mtq.FP8_DEFAULT_CFG, calib_loop)

@@ -42,7 +42,7 @@ def main():
     from modelopt_amd.torch.quantization.config import QuantizeConfig
     from modelopt_amd.torch.quantization.conversion import convert_to_quantized_model
     from modelopt_amd.torch.quantization.nn.modules.tensor_quantizer import TensorQuantizer
-    from scripts.ptq_llama import build_model
+    from benchmarks.ptq_llama import build_model
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)

@@ -1309,11 +1309,20 @@ constexpr int kHistPatterns = 32768;
 // `bounds`, or c * chunk_elems clipped to n_elems when bounds is null) and owns `bpc` consecutive
 // blocks and the count row counts[c * bins, +bins); element bounds need not fall on vectors, so
 // the two edge vectors of a chunk mask their out-of-chunk halves to the dropped NaN pattern.
+//
+// The launch also finishes the job (one launch per call): every block adds its bins into its
+// chunk's row with device-scope atomics, and the last block to finish (agent-scope counter in
+// the scratch's last word) folds hist[b] = sum_c min(fp32(row_c[b]), 2^24) in chunk order, then
+// zeroes the rows and the counter again -- the scratch is all zero between calls, so no memset
+// and no second launch is needed.
 struct HistChunks {
   const int64_t *bounds;  // [chunks + 1] element offsets (device), or null: uniform chunks
   int64_t chunk_elems;
   int64_t n_elems;
   int bpc;  // blocks per chunk
+  int chunks;
+  uint32_t *rows;  // [chunks, bins] counts, then the block counter; zero on entry and on exit
+  float *hist;     // [bins] fp32 result
 };
 
 template <typename T, int U, bool PF, bool CHUNKED = false>
@@ -1471,6 +1480,30 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   __syncthreads();
   for (int b = threadIdx.x; b < bins; b += kHistValThreads)
     if (bh[b]) atomicAdd(counts + b, bh[b]);
+  if constexpr (CHUNKED) {
+    __shared__ bool last;
+    __threadfence();  // this lane's row atomics are device-visible before the block checks in
+    __syncthreads();
+    uint32_t *counter = ch.rows + (int64_t)ch.chunks * bins;
+    if (threadIdx.x == 0) {
+      const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      last = done == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    for (int b = threadIdx.x; b < bins; b += kHistValThreads) {
+      float h = 0.f;
+      for (int c = 0; c < ch.chunks; ++c) {
+        uint32_t *r = ch.rows + (int64_t)c * bins + b;
+        const uint32_t v = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h += fminf((float)v, 16777216.f);
+        __hip_atomic_store(r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ch.hist[b] = h;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ============================================================================================
@@ -2816,18 +2849,6 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
   });
 }
 
-// hist[b] = sum over chunks c, in chunk order, of min(fp32(counts[c][b]), 2^24): torch.histc's
-// per-thread fp32 histograms (a counter stops at 2^24) added in thread order
-__global__ __launch_bounds__(kThreads) void hist_chunk_sum_kernel(const uint32_t *__restrict__ counts,
-                                                                  int chunks, int bins,
-                                                                  float *__restrict__ hist) {
-  const int b = blockIdx.x * kThreads + threadIdx.x;
-  if (b >= bins) return;
-  float h = 0.f;
-  for (int c = 0; c < chunks; ++c) h += fminf((float)counts[(int64_t)c * bins + b], 16777216.f);
-  hist[b] = h;
-}
-
 int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                               int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
                               uint32_t *scratch, float *hist, hipStream_t stream) {
@@ -2836,7 +2857,6 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
   if (!bounds && (chunk_elems < 1 || (chunks - 1) * chunk_elems >= n)) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
   if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
-  if (hipMemsetAsync(scratch, 0, (size_t)chunks * bins * 4, stream) != hipSuccess) return MTQ_ERR_LAUNCH;
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
     if constexpr (sizeof(T) == 2) {
@@ -2855,12 +2875,9 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
       }
-      const HistChunks ch{bounds, chunk_elems, n, (int)bpc};
+      const HistChunks ch{bounds, chunk_elems, n, (int)bpc, chunks, scratch, hist};
       kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
                                                                       hmax, bins, skip_zeros, scratch, ch);
-      if (check_launch() != MTQ_OK) return MTQ_ERR_LAUNCH;
-      hist_chunk_sum_kernel<<<(unsigned)((bins + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-          scratch, chunks, bins, hist);
       return check_launch();
     }
     return MTQ_ERR_DTYPE;

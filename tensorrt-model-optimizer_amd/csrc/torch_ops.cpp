@@ -922,7 +922,8 @@ void histogram_abs_accumulate(const at::Tensor &inputs, const at::Tensor &hmax, 
 
 at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hmax, int64_t bins,
                                  bool skip_zeros, const c10::optional<at::Tensor> &bounds,
-                                 int64_t chunk_elems, int64_t chunks) {
+                                 int64_t chunk_elems, int64_t chunks,
+                                 const c10::optional<at::Tensor> &scratch_in) {
   at::Tensor x = inputs.contiguous();
   check_device(x, "inputs");
   TORCH_CHECK(hmax.scalar_type() == at::kFloat && hmax.numel() == 1, "histogram: hmax fp32 scalar");
@@ -936,7 +937,17 @@ at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hma
     bp = b.data_ptr<int64_t>();
   }
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  at::Tensor scratch = at::empty({chunks, bins}, x.options().dtype(at::kInt));
+  // all-zero [chunks * bins + 1] int32, left all zero by the launch: the caller's reusable one, or
+  // a fresh one
+  at::Tensor scratch;
+  if (scratch_in.has_value() && scratch_in->defined()) {
+    scratch = *scratch_in;
+    TORCH_CHECK(scratch.scalar_type() == at::kInt && scratch.is_contiguous() && scratch.device() == x.device() &&
+                    scratch.numel() >= chunks * bins + 1,
+                "histogram_abs_chunked: scratch must be contiguous int32 [>= chunks * bins + 1] on the input's device");
+  } else {
+    scratch = at::zeros({chunks * bins + 1}, x.options().dtype(at::kInt));
+  }
   at::Tensor hist = at::empty({bins}, x.options().dtype(at::kFloat));
   int st = mtq_histogram_abs_chunked(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"),
                                      hmax.data_ptr<float>(), (int)bins, skip_zeros ? 1 : 0, bp,
@@ -1082,7 +1093,7 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
         "bool skip_zeros) -> ()");
   m.def("histogram_abs_chunked(Tensor inputs, Tensor hmax, int bins, bool skip_zeros, Tensor? bounds, "
-        "int chunk_elems, int chunks) -> Tensor");
+        "int chunk_elems, int chunks, Tensor(a!)? scratch=None) -> Tensor");
   m.def("qlinear_small_m_group(Tensor[] inputs, Tensor[] weights, Tensor?[] biases, Tensor[] amaxs, int[] blocks, "
         "int kind, int[] num_bits, int[] is_unsigned, int[] narrow_range) -> Tensor[]");
   m.def("qlinear_small_m(Tensor input, Tensor weight, Tensor? bias, Tensor amax, int block, int kind, "

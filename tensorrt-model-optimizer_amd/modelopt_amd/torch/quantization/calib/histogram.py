@@ -143,6 +143,19 @@ _HISTC_GRAIN = 32768  # at::internal::GRAIN_SIZE: the parallel_for grain of the 
 _F32_COUNT_LIMIT = 2**24  # an fp32 counter stops here: 2^24 + 1 rounds to 2^24 (ties to even)
 
 
+# All-zero int32 scratch of the one-launch chunked histogram (the launch leaves it zero again),
+# one per (device, stream): calls on one stream are ordered, so they can share it.
+_CHUNK_SCRATCH: dict = {}
+
+
+def _chunk_scratch(device: torch.device, words: int) -> torch.Tensor:
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    buf = _CHUNK_SCRATCH.get(key)
+    if buf is None or buf.numel() < words:
+        buf = _CHUNK_SCRATCH[key] = torch.zeros(max(words, 16 * 8192 + 1), dtype=torch.int32, device=device)
+    return buf
+
+
 def _histc_threads() -> int:
     env = os.environ.get("MTQ_AMD_HIST_THREADS")
     return max(1, int(env)) if env else max(1, torch.get_num_threads())
@@ -156,7 +169,7 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T = threads``,
     default ``_histc_threads()``; chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted
     exactly, clamped at 2^24 and added into the fp32 result in thread order: bf16 / f16 on the GPU
-    in two launches for all chunks (histogram_abs_chunked), other inputs one launch per chunk."""
+    in one launch for all chunks (histogram_abs_chunked), other inputs one launch per chunk."""
     ops = _ops()
     n = x.numel()
     mode = os.environ.get("MTQ_AMD_HIST_COUNTS", "histc")
@@ -184,13 +197,18 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
         cuts = torch.searchsorted(csum, torch.tensor(starts[1:-1], device=csum.device, dtype=torch.int64) + 1)
     if (flat.is_cuda and flat.dtype in (torch.bfloat16, torch.float16) and bins <= 8192 and n % 8 == 0
             and flat.data_ptr() % 16 == 0):
-        # one launch counts every chunk into its own row, a second adds the clamped rows in order
+        # one launch counts every chunk into its own row; its last workgroup adds the clamped rows in order
         nch = len(starts) - 1
         dev_bounds = None
         if cuts is not None:
             z = torch.zeros(1, dtype=torch.int64, device=flat.device)
             dev_bounds = torch.cat([z, cuts, torch.full_like(z, n)])
-        return ops.histogram_abs_chunked(flat, hmax, bins, skip_zeros, dev_bounds, chunk, nch)
+        scratch = _chunk_scratch(flat.device, nch * bins + 1)
+        try:
+            return ops.histogram_abs_chunked(flat, hmax, bins, skip_zeros, dev_bounds, chunk, nch, scratch)
+        except Exception:
+            _CHUNK_SCRATCH.clear()  # a failed launch may leave it non-zero
+            raise
     bounds = [0] + cuts.tolist() + [n] if cuts is not None else starts
     hist = torch.zeros(bins, dtype=torch.float32, device=x.device)
     counts = torch.empty(bins, dtype=torch.int32, device=x.device)

@@ -81,7 +81,7 @@ def finish_stats_collection(model: nn.Module, method: str | None = None, **kwarg
             continue
         cal = getattr(module, "_calibrator", None)
         if cal and not getattr(module, "_dynamic", False):
-            if method is None and not kwargs and type(cal) is MaxCalibrator:
+            if method is None and not kwargs and type(cal) is MaxCalibrator and type(module) is TensorQuantizer:
                 # load_calib_amax's steps with the amax computed once (its fp32 -> dtype cast is a
                 # fresh tensor: adopted without the setter's copy)
                 amax = cal.compute_amax()
@@ -271,12 +271,19 @@ _act_scale_memo = [None, None, None]  # weakref to the tensor, its _version, the
 
 
 def _act_scale_shared(x):
+    if x.is_inference():
+        # inference tensors (torch.inference_mode) carry no version counter to key the memo on
+        return get_act_scale(x)
     ref, ver, val = _act_scale_memo
     if ref is not None and ref() is x and ver == x._version:
         return val
     val = get_act_scale(x)
     _act_scale_memo[:] = [weakref.ref(x), x._version, val]
     return val
+
+
+def _act_scale_memo_clear():
+    _act_scale_memo[:] = [None, None, None]
 
 
 def get_scale(x_max, w_max, alpha, tensor_parallel_group=None):
@@ -389,6 +396,8 @@ def _mse_fast(out, ref) -> bool:
 _AWQ_FUSED_MAX_N = 2048
 _AWQ_FUSED_MAX_G = 64
 _AWQ_FUSED = os.environ.get("MTQ_AMD_AWQ_FUSED", "auto")
+if _AWQ_FUSED not in ("auto", "always", "library", "never"):
+    raise ValueError(f"MTQ_AMD_AWQ_FUSED={_AWQ_FUSED!r}: expected auto, always, library or never")
 # Budget for keeping every alpha's quantised weight [11, N, K] across the search batches (it does
 # not change between batches; the reference recomputes it per batch): a fraction of the HBM free
 # when the search pass starts (Llama-3-8B: 154 GB of 288 GB).
@@ -444,8 +453,6 @@ def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
     # batched path's loss pass takes G <= 16; anything else runs one alpha at a time
     fused_ok = n_alpha <= _AWQ_FUSED_MAX_G and x2.shape[0] * k_in < 2**31 and n_out * k_in < 2**31
     fused = fused_ok and (_AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and n_out <= _AWQ_FUSED_MAX_N))
-    if _AWQ_FUSED not in ("auto", "always", "library"):
-        raise ValueError(f"MTQ_AMD_AWQ_FUSED={_AWQ_FUSED!r}: expected auto, always, library or never")
     if fused:
         ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
     elif n_alpha <= 16:
@@ -710,7 +717,10 @@ def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.
 
     _AWQLiteHelper.cache_mode = True
     enable_stats_collection(model)
-    forward_loop(model)
+    try:
+        forward_loop(model)
+    finally:
+        _act_scale_memo_clear()  # the last act scale is not kept alive past the caching pass
     with set_quantizer_by_cfg_context(model, [{"quantizer_name": "*weight_quantizer", "enable": False}]):
         max_calibrate(model, lambda m: None, distributed_sync=True)
     finish_stats_collection(model)

@@ -532,9 +532,10 @@ class TensorQuantizer(nn.Module):
         acc = getattr(calibrator, "_acc", None)
         if acc is not None and amax.untyped_storage().data_ptr() == acc.untyped_storage().data_ptr():
             amax = amax.clone()
-        if "_amax" not in self._buffers:
+        if "_amax" not in self._buffers and type(self) is TensorQuantizer:
             self.register_buffer("_amax", amax.detach())
         else:
+            # subclasses keep their setter semantics (StaticBlockScaleQuantizer: fp32 amax)
             self._amax_setter_helper(amax)
 
     def _get_amax(self, inputs):
@@ -771,6 +772,18 @@ class TensorQuantizer(nn.Module):
             elif isinstance(self.axis, int) or (isinstance(self.axis, (list, tuple)) and len(self.axis) == 1):
                 amax = amax.squeeze()
         return amax
+
+    def returns_input_unchanged(self) -> bool:
+        """``forward(x)`` returns ``x`` itself for a plain tensor ``x``: disabled, or collect-only
+        calibration (no fake quant, not dynamic), with no pre_quant_scale and no block reshape.
+        Callers may then launch the consumer of ``x`` before calling the quantizer."""
+        d = self.__dict__
+        if d["_disabled"]:
+            return self.pre_quant_scale is None
+        return (
+            d["_if_calib"] and not d["_if_quant"] and not d["_dynamic"] and d.get("_block_sizes") is None
+            and self.pre_quant_scale is None
+        )
 
     # ---- forward --------------------------------------------------------------------------------
     def forward(self, inputs):

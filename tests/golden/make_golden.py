@@ -20,6 +20,9 @@ Outputs (small; committed):
   llama_fp8.safetensors      C2 class: tiny LlamaForCausalLM FP8_DEFAULT_CFG PTQ (amax + logits)
   awq.safetensors/.json      C3 class: awq_lite on a small MLP (best alpha/scale, weights, amax)
   awq_b128.safetensors/.json C3 proper: INT4_AWQ_CFG (block 128) in bf16 on K % 128 == 0 linears
+  prod.safetensors/.json     E2E at production shapes: 2-layer Llama-3-8B-shaped FP8 / INT8 / INT4-AWQ
+                             and a hidden-1024 8-expert Mixtral layer FP8 (amax, AWQ scales, logits;
+                             weights regenerated from the seed, pinned by sha256)
   presets.json               the reference preset configs
   mx_kat.json                the MX known-answer tables of test_quantize_mxformats_cuda.py (data)
 """
@@ -359,6 +362,64 @@ def gen_mixtral_fp8():
                 t[f"amax.{n}"] = q.amax.clone().contiguous()
     save_file(t, str(OUT / "mixtral_fp8.safetensors"))
     (OUT / "mixtral_fp8.json").write_text(json.dumps({"quantizers": names}, indent=0))
+
+
+sys.path.insert(0, str(OUT))
+from prod_models import PROD_CASES, fingerprint as _fingerprint, prod_inputs, prod_model, sha as _sha  # noqa: E402
+
+
+def _prod_case(kind, seed, cfg_name, algorithm=None):
+    import copy
+
+    model = prod_model(kind, seed)
+    fp = _fingerprint(model)
+    ids, test = prod_inputs(seed)
+    cfg = copy.deepcopy(getattr(mtq, cfg_name))
+    if algorithm is not None:
+        cfg["algorithm"] = algorithm
+
+    def loop(mm):
+        for b in ids:
+            mm(b)
+
+    with torch.no_grad():
+        mtq.quantize(model, cfg, loop)
+        logits = model(test).logits.float()
+    t = {"calib_ids": ids, "test_ids": test, "logits": logits}
+    meta = {"kind": kind, "seed": seed, "config": cfg_name, "algorithm": algorithm, "fingerprint": fp,
+            "threads": torch.get_num_threads(), "amax_sha": {}, "weight_sha": {}, "awq": {}}
+    for n, q in model.named_modules():
+        if isinstance(q, TensorQuantizer) and q.is_enabled and q.amax is not None:
+            a = q.amax.detach()
+            if a.numel() <= 65536:
+                t[f"amax.{n}"] = a.clone().contiguous()
+            else:  # static block amax (INT4 block 128: 1.8 M values per layer): bytes pinned by hash
+                meta["amax_sha"][n] = [_sha(a), str(a.dtype), list(a.shape)]
+    for n, m in model.named_modules():
+        if hasattr(m, "awq_lite"):
+            h = m.awq_lite
+            meta["awq"][n] = {"best_alpha": h.best_alpha, "N": m.weight.shape[0], "K": m.weight.shape[1]}
+            t[f"act_scale.{n}"] = h.act_scale.clone()
+            t[f"best_scale.{n}"] = h.best_scale.clone()
+            meta["weight_sha"][n] = _sha(m.weight)
+    return t, meta
+
+
+def gen_prod():
+    """End-to-end parity at production dispatch sizes: mtq.quantize on a
+    2-layer Llama with Llama-3-8B layer shapes (hidden 4096, intermediate 14336, 32 / 8 heads) under
+    FP8_DEFAULT_CFG (per-tensor), INT8_DEFAULT_CFG (per-channel weights) and INT4_AWQ_CFG (awq_lite,
+    block 128), and a 1-layer Mixtral (hidden 1024, 8 experts) under FP8_DEFAULT_CFG, in bf16.
+    Weights are regenerated from the seed (their sha256 is stored), so only inputs, amax, AWQ
+    scales and logits are kept."""
+    tensors, meta = {}, {}
+    for name, (kind, seed, cfg_name, algo) in PROD_CASES.items():
+        print("  prod case", name, flush=True)
+        t, m = _prod_case(kind, seed, cfg_name, algo)
+        tensors.update({f"{name}.{k}": v for k, v in t.items()})
+        meta[name] = m
+    save_file(tensors, str(OUT / "prod.safetensors"))
+    (OUT / "prod.json").write_text(json.dumps(meta, indent=0))
 
 
 class _SimpleMLP(nn.Module):

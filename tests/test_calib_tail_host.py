@@ -61,3 +61,31 @@ def test_validate_attrs_warns_on_negative_amax():
         warnings.simplefilter("always")
         _validate_quantizer_attrs(nn.ModuleDict({"ok": holder.ok}))
     assert not w
+
+
+def test_static_block_quantizer_recalibrated_keeps_fp32_amax():
+    """A promoted StaticBlockScaleQuantizer max-calibrated again after reset_amax keeps its amax
+    in fp32 (its _amax_setter_helper override), not in the input dtype."""
+    import torch
+    import torch.nn as nn
+
+    import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization.nn.modules.tensor_quantizer import StaticBlockScaleQuantizer
+
+    cfg = {
+        "quant_cfg": [
+            {"quantizer_name": "*", "enable": False},
+            {"quantizer_name": "*weight_quantizer", "cfg": {"num_bits": 4, "block_sizes": {-1: 8, "type": "static"}}},
+        ],
+        "algorithm": "max",
+    }
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(16, 16)).to(torch.bfloat16)
+    mtq.quantize(m, cfg, lambda mm: mm(torch.randn(4, 16, dtype=torch.bfloat16)))
+    q = m[0].weight_quantizer
+    assert isinstance(q, StaticBlockScaleQuantizer) and q._amax.dtype == torch.float32
+    q.reset_amax()
+    mtq.calibrate(m, "max", lambda mm: mm(torch.randn(4, 16, dtype=torch.bfloat16)))
+    assert q._amax.dtype == torch.float32
+    want = m[0].weight.detach().float().view(-1, 8).abs().amax(dim=1, keepdim=True)
+    assert torch.equal(q._amax.view(-1, 1), want)

@@ -22,3 +22,16 @@ def test_every_env_switch_is_documented():
     assert len(used) <= 10, sorted(used)
     documented = set(re.findall(r"`(MTQ_AMD_[A-Z0-9_]+)`", table)) - {"MTQ_AMD_DIST_BACKEND"}
     assert documented <= used, sorted(documented - used)
+
+
+def test_awq_fused_switch_validated_at_import():
+    """A misspelt MTQ_AMD_AWQ_FUSED fails at import, not only on the fused search path."""
+    import os
+    import subprocess
+    import sys
+
+    env = {**os.environ, "MTQ_AMD_AWQ_FUSED": "alwyas",
+           "PYTHONPATH": os.pathsep.join([str(REPO / "tensorrt-model-optimizer_amd"), str(REPO)])}
+    r = subprocess.run([sys.executable, "-c", "import modelopt_amd.torch.quantization"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "MTQ_AMD_AWQ_FUSED='alwyas'" in r.stderr, r.stderr[-2000:]

@@ -165,3 +165,24 @@ def test_histc_chunked_single_launch_matches_per_chunk_counts(gpu, dtype):
     y = torch.full((F32 + 64,), 0.25, dtype=dtype, device=gpu)
     got = ops.histogram_abs_chunked(y, hmax, 2048, False, None, F32 + 64, 1)
     assert float(got.max()) == float(F32) and float(got.sum()) == float(F32)
+
+
+def test_histc_chunked_scratch_left_zero_and_reusable(gpu):
+    """The one-launch chunked histogram leaves its scratch (rows + block counter) all zero, so one
+    buffer serves every call on a stream: back-to-back calls with varying chunk counts / bins on
+    one scratch give the results of fresh-scratch calls."""
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    g = torch.Generator(device=gpu).manual_seed(5)
+    n = 8 * 1_500_001
+    x = (torch.randn(n, device=gpu, generator=g) * 3).to(torch.bfloat16)
+    hmax = torch.tensor([8.0], device=gpu)
+    scratch = torch.zeros(16 * 4096 + 1, dtype=torch.int32, device=gpu)
+    for chunks, bins in ((16, 2048), (3, 4096), (7, 1000), (16, 2048)):
+        chunk = -(-n // chunks)
+        fresh = ops.histogram_abs_chunked(x, hmax, bins, False, None, chunk, chunks)
+        for _ in range(2):
+            got = ops.histogram_abs_chunked(x, hmax, bins, False, None, chunk, chunks, scratch)
+            assert torch.equal(got, fresh), (chunks, bins)
+            assert int(scratch.abs().sum()) == 0, "scratch not left zero"
