@@ -410,6 +410,16 @@ int mtq_attention_fwd(const void *q, const void *k, const void *v, void *o,
                       const int64_t *strides, int is_causal, double softmax_scale,
                       int p_qdq_mode, double p_qdq_scale, int dtype, hipStream_t stream);
 
+/* ---- dispatch registry (tracing) ----------------------------------------------------------
+ * The launchers choose among kernel forms by shape, dtype and alignment (vector / block-group /
+ * row-wave fake quant, persistent / row / column amax, ...); each launch of the families below
+ * bumps a process-wide counter (one relaxed atomic add on the host).  mtq_dispatch_counts copies
+ * min(n, count) counters into `counts` and returns the number of families; mtq_dispatch_name(i)
+ * is family i's name (NULL out of range).  Used by the production-shape parity tests to prove
+ * which kernels a Llama-shaped mtq.quantize reaches; no reference counterpart (tracing aux). */
+int mtq_dispatch_counts(int64_t *counts, int n);
+const char *mtq_dispatch_name(int id);
+
 #ifdef __cplusplus
 }
 #endif

@@ -416,6 +416,7 @@ void launch_prescale(const void *x, const void *sinv, void *xs, int64_t M, int64
   const T *xt = reinterpret_cast<const T *>(x);
   const T *st = reinterpret_cast<const T *>(sinv);
   T *ot = reinterpret_cast<T *>(xs);
+  count_dispatch(kDispAwqPrescale);
   if (G == 11)  // alpha_step 0.1, the awq_lite default
     awq_prescale_kernel<T, 11><<<gb, 256, 0, stream>>>(xt, st, ot, chunks, K / 8, G);
   else
@@ -518,6 +519,7 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
   // 32 slots per 8 x 4 tile unit, units padded to a multiple of the 8 XCDs (see the kernel)
   const int64_t units = (int64_t)G * ((tiles_m + 7) / 8) * ((tiles_n + 3) / 4);
   const dim3 grid((unsigned)((units + 7) / 8 * 8 * 32));
+  count_dispatch(kDispAwqSearchPp);
   if (dtype == MTQ_BF16) {
     if (bias)
       awq_search_pp_kernel<__bf16, true><<<grid, kThreads, 0, stream>>>(a);
@@ -551,6 +553,7 @@ extern "C" int mtq_awq_mse_multi(const void *out, const void *ref, int64_t n, in
   if (!al16(out) || !al16(ref)) return MTQ_ERR_INVALID_ARG;
   const int64_t grid = mtq_awq_mse_multi_workspace_floats(n, G) / G;
   if (workspace_floats < grid * G) return MTQ_ERR_INVALID_ARG;
+  count_dispatch(kDispAwqMseMulti);
   if (dtype == MTQ_BF16)
     awq_mse_multi_kernel<__bf16><<<(unsigned)grid, 256, 0, stream>>>((const __bf16 *)out, (const __bf16 *)ref,
                                                                     n / 8, G, workspace);

@@ -410,4 +410,16 @@ __device__ __forceinline__ uint32_t fmod_(uint32_t n, uint32_t q, const FastDiv 
   return n - q * f.d;
 }
 
+// ---- dispatch registry (host side): one relaxed atomic increment per launch of the kernel
+// families below, read through mtq_dispatch_counts (which kernel a call reached is otherwise
+// invisible to a caller: the launchers pick among vector / group / row-wave / persistent forms
+// by shape and alignment).  Names in mtq_dispatch_name; the order is the ABI.
+enum DispatchId {
+  kDispEwVec, kDispEwGroupSk, kDispEwGroup, kDispEwRowwave, kDispAmaxPersist, kDispAmaxRowsU,
+  kDispAmaxRowsShort, kDispAmaxColsWide, kDispBlockQuantDyn, kDispHistValue, kDispHistValueChunked,
+  kDispMxVec, kDispMxE2m1Native, kDispNvfp4NativeU, kDispAwqSearchPp, kDispAwqPrescale, kDispAwqMseMulti,
+  kDispCount
+};
+void count_dispatch(int id);
+
 }  // namespace mtq

@@ -8,6 +8,7 @@
 // unlike tensor_quant_gpu_fp8.cu:97-100), and wave64 shuffle reductions.  Reference citations
 // are relative to the reference repository root.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <string.h>
 #include <math.h>
@@ -126,6 +127,7 @@ int launch_ew(const void *xv, void *yv, int64_t n, Op op, hipStream_t stream) {
   int64_t nvec = (aligned16(x) && aligned16(y)) ? n / N : 0;
   if (nvec > 0) {
     const unsigned blocks = (unsigned)((nvec + kThreads - 1) / kThreads);
+    count_dispatch(kDispEwVec);
     ew_vec_kernel<T, Op, 1, true><<<blocks, kThreads, 0, stream>>>(x, y, nvec, op);
   }
   int64_t done = nvec * N;
@@ -452,6 +454,7 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
       if (nvec > 0 && sk) {
         auto go = [&](auto lc) {
           constexpr int L = decltype(lc)::value;
+          count_dispatch(kDispEwGroupSk);
           ew_group_sk_kernel<T, VecOp<T>, U, L><<<g, kThreads, 0, stream>>>(
               reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
               reinterpret_cast<const float *>(op.amax), axis_size, op);
@@ -463,6 +466,7 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
         else
           go(std::integral_constant<int, 32>{});
       } else if (nvec > 0)
+        count_dispatch(kDispEwGroup);
         ew_group_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec, (int)(vb / U), op);
       const int64_t done = nvec * N;
@@ -481,6 +485,7 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
       const int64_t nvec = n / N;
       const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
       if (nvec > 0)
+        count_dispatch(kDispEwRowwave);
         ew_rowwave_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
             reinterpret_cast<const float *>(op.amax), vb, op);
@@ -645,6 +650,7 @@ void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t strea
   const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
   if constexpr (sizeof(T) == 2) {
     if (p.fmt == MTQ_E2M1 && p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
+      count_dispatch(kDispMxE2m1Native);
       mx_e2m1_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec);
       return;
     }
@@ -652,6 +658,7 @@ void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t strea
   const unsigned g2 = (unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads));
   auto go = [&](auto fmt_c) {
     constexpr int F = decltype(fmt_c)::value;
+    count_dispatch(kDispMxVec);
     mx_vec_kernel<T, BS, F, 2><<<g2, kThreads, 0, stream>>>(x, y, nvec, p);
   };
   switch (p.fmt) {
@@ -825,6 +832,7 @@ int launch_amax_persist(const T *x, int64_t n, int64_t nvec, uint32_t *out, int 
   const int64_t cap = (int64_t)num_cus() * per_cu;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
+  count_dispatch(kDispAmaxPersist);
   amax_persist_kernel<T, U><<<(unsigned)blocks, kAmaxThreads, 0, stream>>>(x, n, nvec, out);
   return check_launch();
 }
@@ -1045,6 +1053,7 @@ int launch_amax_cols_wide(const T *x, int64_t P, int64_t K, uint32_t *out, int b
   const int64_t rows_per_slab = (P + slabs - 1) / slabs;
   slabs = (P + rows_per_slab - 1) / rows_per_slab;
   const unsigned g = (unsigned)(nchunks * slabs);
+  count_dispatch(kDispAmaxColsWide);
   amax_cols_wide_kernel<T, U><<<g, kColsThreads, 0, stream>>>(x, P, K, lpr, nchunks,
                                                               rows_per_slab, out);
   return check_launch();
@@ -1100,6 +1109,7 @@ int launch_amax_rows_u(const T *x, int64_t P, int64_t K, int64_t Q, uint32_t *ou
     const int64_t chunks = (qvec + G * U - 1) / (G * U);
     const int64_t items = R * chunks;
     const unsigned g = (unsigned)((items + kThreads / G - 1) / (kThreads / G));
+    count_dispatch(kDispAmaxRowsU);
     if (chunks == 1 && P == 1)
       amax_rows_u_kernel<T, G, U, true><<<g, kThreads, 0, stream>>>(x, R, Q, K, chunks, out);
     else
@@ -1112,6 +1122,7 @@ int launch_amax_rows_u(const T *x, int64_t P, int64_t K, int64_t Q, uint32_t *ou
     constexpr int G = decltype(gtag)::value;
     const int64_t rows_per_block = (int64_t)(kThreads / G) * RU;
     const unsigned g = (unsigned)((R + rows_per_block - 1) / rows_per_block);
+    count_dispatch(kDispAmaxRowsShort);
     if (P == 1)
       amax_rows_short_kernel<T, G, RU, true><<<g, kThreads, 0, stream>>>(x, R, Q, K, out);
     else
@@ -1481,17 +1492,21 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   for (int b = threadIdx.x; b < bins; b += kHistValThreads)
     if (bh[b]) atomicAdd(counts + b, bh[b]);
   if constexpr (CHUNKED) {
-    __shared__ bool last;
-    __threadfence();  // this lane's row atomics are device-visible before the block checks in
+    // (the flag lives in the dynamic LDS, free again here: a static __shared__ variable would
+    // push static + dynamic LDS past the 160 KiB the launch reserves)
+    // this wave's row atomics performed (workgroup-scope release: a vscnt / vmcnt wait, no L2
+    // writeback -- a device-scope fence in every lane cost more than the whole count), then one
+    // device-scope acq_rel check-in per block
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     uint32_t *counter = ch.rows + (int64_t)ch.chunks * bins;
     if (threadIdx.x == 0) {
       const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      last = done == gridDim.x - 1;
+      sh[0] = done == gridDim.x - 1 ? 1u : 0u;
     }
     __syncthreads();
-    if (!last) return;
-    __threadfence();
+    if (!sh[0]) return;
+    // the rows are read and cleared with device-scope atomic loads / stores (past the caches)
     for (int b = threadIdx.x; b < bins; b += kHistValThreads) {
       float h = 0.f;
       for (int c = 0; c < ch.chunks; ++c) {
@@ -1757,6 +1772,7 @@ int launch_nvfp4(const T *x, T *y, int64_t rows, int64_t cols, const float *gama
     const int64_t nvec = rows * cols / N;
     const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
     if constexpr (sizeof(T) == 2) {
+      count_dispatch(kDispNvfp4NativeU);
       nvfp4_native_u_kernel<T, BS, 2><<<(unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0,
                                         stream>>>(x, y, nvec, gamax);
       return check_launch();
@@ -2580,12 +2596,26 @@ __global__ __launch_bounds__(kThreads) void export_mxfp8_kernel(const T *__restr
 namespace mtq {
 int host_check_launch() { return check_launch(); }
 int host_num_cus() { return num_cus(); }
+static std::atomic<long long> g_dispatch[kDispCount];
+void count_dispatch(int id) { g_dispatch[id].fetch_add(1, std::memory_order_relaxed); }
+static const char *const kDispatchNames[kDispCount] = {
+    "ew_vec", "ew_group_sk", "ew_group", "ew_rowwave", "amax_persist", "amax_rows_u", "amax_rows_short",
+    "amax_cols_wide", "block_quant_dyn", "hist_value", "hist_value_chunked", "mx_vec", "mx_e2m1_native",
+    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi"};
 }  // namespace mtq
 
 // ============================================================================================
 // C ABI
 // ============================================================================================
 extern "C" {
+
+int mtq_dispatch_counts(int64_t *counts, int n) {
+  if (n < 0 || (n > 0 && !counts)) return -1;
+  for (int i = 0; i < n && i < kDispCount; ++i) counts[i] = g_dispatch[i].load(std::memory_order_relaxed);
+  return kDispCount;
+}
+
+const char *mtq_dispatch_name(int id) { return id >= 0 && id < kDispCount ? kDispatchNames[id] : nullptr; }
 
 const char *mtq_status_string(int status) {
   switch (status) {
@@ -2762,6 +2792,7 @@ int mtq_block_quant_dynamic(const void *x, void *y, int64_t rows, int64_t cols, 
     auto go_u = [&](auto blk_c) {
       constexpr int BLK = decltype(blk_c)::value, U = 2;
       const unsigned gu = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
+      count_dispatch(kDispBlockQuantDyn);
       block_quant_dyn_kernel<T, BLK, U><<<gu, kThreads, 0, stream>>>(xt, yt, pt, nvec, cols, b.max_bound, b.min_bound);
     };
     switch (block) {
@@ -2809,6 +2840,7 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
           attr = true;
         }
+        count_dispatch(kDispHistValue);
         kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins, skip_zeros, counts,
                                                                     HistChunks{});
         return check_launch();
@@ -2876,6 +2908,7 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
         attr = true;
       }
       const HistChunks ch{bounds, chunk_elems, n, (int)bpc, chunks, scratch, hist};
+      count_dispatch(kDispHistValueChunked);
       kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
                                                                       hmax, bins, skip_zeros, scratch, ch);
       return check_launch();

@@ -72,6 +72,20 @@ def kernel_cdll() -> ctypes.CDLL:
     return _state["cdll"]
 
 
+def dispatch_counts() -> dict[str, int]:
+    """Launches per kernel family since the library was loaded (``mtq_dispatch_counts``: the
+    launchers pick vector / block-group / row-wave / persistent forms by shape; this shows which
+    ones a workload reached).  Take two snapshots and subtract to scope it to a region."""
+    _load_ops()  # the op library's copy of libmtq_amd.so is the one that launches
+    lib = kernel_cdll()
+    lib.mtq_dispatch_name.restype = ctypes.c_char_p
+    lib.mtq_dispatch_name.argtypes = [ctypes.c_int]
+    n = lib.mtq_dispatch_counts(None, 0)
+    buf = (ctypes.c_int64 * n)()
+    lib.mtq_dispatch_counts(buf, n)
+    return {lib.mtq_dispatch_name(i).decode(): int(buf[i]) for i in range(n)}
+
+
 def declared_symbols(header: Path = HEADER) -> list[str]:
     """Function names declared in include/mtq_amd.h."""
     text = header.read_text()

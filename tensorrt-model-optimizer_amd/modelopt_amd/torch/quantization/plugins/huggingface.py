@@ -82,11 +82,6 @@ class _QuantFusedExperts(QuantModule):
         args = list(args)
         hs = args[0] if args else kwargs.get("hidden_states")
         idx_t = args[1] if len(args) > 1 else kwargs.get("top_k_index")
-        # Calibration collects whose quantizer hands its input back unchanged run on a side
-        # stream (``_collect_beside``): they only read their input, so the expert loop's next
-        # kernels need not wait for them.  The main stream joins the side stream before this
-        # forward returns, so every reader of the running maxima is ordered after them.
-        side = None
         if (
             isinstance(hs, torch.Tensor) and hs.dim() == 2 and isinstance(idx_t, torch.Tensor)
             and idx_t.dim() == 2 and idx_t.shape[0] == hs.shape[0] and _token_separable(first_in)
@@ -95,73 +90,65 @@ class _QuantFusedExperts(QuantModule):
                 # one library pass (no compare / any / where kernels to load on first use)
                 from modelopt_amd._ext import ops as _ops
 
-                if first_in.returns_input_unchanged():
-                    # collect only: the experts may read hs itself (rows routed to no local
-                    # expert are never gathered), the masked copy feeds the collect alone
-                    side = _side_stream(hs.device)
-                    with _beside(side, hs, idx_t):
-                        first_in(_ops().mask_unrouted_rows(hs, idx_t, self.num_experts))
-                else:
-                    hs = first_in(_ops().mask_unrouted_rows(hs, idx_t, self.num_experts))
+                masked = first_in(_ops().mask_unrouted_rows(hs, idx_t, self.num_experts))
             else:
                 routed = ((idx_t >= 0) & (idx_t < self.num_experts)).any(dim=-1, keepdim=True)
-                hs = first_in(torch.where(routed, hs, hs.new_zeros(())))
-            if args:
-                args[0] = hs
-            else:
-                kwargs["hidden_states"] = hs
+                masked = first_in(torch.where(routed, hs, hs.new_zeros(())))
+            if not first_in.returns_input_unchanged():
+                # fake quant: the experts read the quantised tokens (a collect-only call hands
+                # back the masked copy itself: the experts read hs, whose unrouted rows no
+                # expert gathers)
+                if args:
+                    args[0] = masked
+                else:
+                    kwargs["hidden_states"] = masked
             d["_first_in_done"] = True
-        if side is None and isinstance(hs, torch.Tensor) and hs.is_cuda:
-            side = _side_stream(hs.device)
+        # The eager expert loop syncs the host once per expert (torch.where, and the expert-index
+        # slice of the fused weight), so host time between such a sync and the next GEMM launch
+        # is GPU idle time.  Quantizers that hand their input back unchanged (calibration collect,
+        # no fake quant) are therefore called AFTER the GEMM is launched -- the same calls on the
+        # same tensors, their host time behind the GEMM -- and whether they do is decided once
+        # per forward here, not per expert.
+        first_late = d["_first_in_done"] and all(_returns_input_q(q) for q in first_w)
+        down_late = _returns_input_q(self.down_proj_input_quantizer) and all(
+            _returns_input_q(q) for q in self.down_proj_weight_quantizers)
 
         def _quantized_linear(input, weight, bias=None):
-            # The eager expert loop syncs the host once per expert (torch.where, and the
-            # expert-index slice of the fused weight), so the host time between that sync and
-            # this GEMM's launch is GPU idle time.  Quantizers that hand their input back
-            # unchanged (calibration collect, no fake quant) are therefore called AFTER the GEMM
-            # is launched: same calls, same collected tensors, their host time behind the GEMM
-            # and their kernels on the side stream.
             if d["_down_proj_linear"]:
                 d["_down_proj_linear"] = False
                 idx = d["_current_expert_idx"]
-                in_q = self.down_proj_input_quantizer
                 wq = self.down_proj_weight_quantizers[idx]
-                if _returns_input(in_q, input) and _returns_input(wq, weight):
+                if down_late and type(input) is torch.Tensor and type(weight) is torch.Tensor:
                     out = orig_linear(input, weight, bias)
-                    if side is not None and input.is_cuda:
-                        with _beside(side, input):
-                            in_q(input)
-                    else:
-                        in_q(input)
+                    self.down_proj_input_quantizer(input)
                     if not _collected_already(wq, weight):
                         wq(weight)
                     return out
-                input = in_q(input)
+                input = self.down_proj_input_quantizer(input)
                 if not _collected_already(wq, weight):
                     weight = wq(weight)
                 return orig_linear(input, weight, bias)
             d["_down_proj_linear"] = True
-            idx = self._get_expert_idx_from_first_proj(weight)
-            d["_current_expert_idx"] = idx
-            wq = first_w[idx]
-            if d["_first_in_done"] and _returns_input(wq, weight):
+            if first_late and type(input) is torch.Tensor and type(weight) is torch.Tensor:
                 out = orig_linear(input, weight, bias)
+                idx = self._get_expert_idx_from_first_proj(weight)
+                d["_current_expert_idx"] = idx
+                wq = first_w[idx]
                 if not _collected_already(wq, weight):
                     wq(weight)
                 return out
+            idx = self._get_expert_idx_from_first_proj(weight)
+            d["_current_expert_idx"] = idx
             if not d["_first_in_done"]:
                 input = first_in(input)
+            wq = first_w[idx]
             if not _collected_already(wq, weight):
                 weight = wq(weight)
             return orig_linear(input, weight, bias)
 
         d["_down_proj_linear"] = False
-        try:
-            with _replace_function(torch.nn.functional, "linear", _quantized_linear):
-                return self._original_cls.forward(self, *args, **kwargs)
-        finally:
-            if side is not None:
-                torch.cuda.current_stream(side.device).wait_stream(side)
+        with _replace_function(torch.nn.functional, "linear", _quantized_linear):
+            return self._original_cls.forward(self, *args, **kwargs)
 
     def iter_weights_for_calibration(self):
         for wname, qname in ((self._first_proj_attr, f"{self._first_proj_attr}_weight_quantizers"),
@@ -189,34 +176,11 @@ def _collected_already(q, weight) -> bool:
     return type(q) is TensorQuantizer and quantizer_call_is_noop(q, weight)
 
 
-_SIDE_STREAMS: dict = {}
-
-
-def _side_stream(device: torch.device) -> torch.cuda.Stream:
-    """The stream (one per device) that runs the MoE plugin's calibration collects beside the
-    expert loop's own kernels."""
-    s = _SIDE_STREAMS.get(device)
-    if s is None:
-        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
-    return s
-
-
-@contextlib.contextmanager
-def _beside(side: torch.cuda.Stream, *inputs: torch.Tensor):
-    """Run the enclosed launches on ``side`` after everything the current stream has queued
-    (which produced ``inputs``); ``inputs`` stay allocated until the side stream has read them."""
-    side.wait_stream(torch.cuda.current_stream(side.device))
-    with torch.cuda.stream(side):
-        yield
-    for t in inputs:
-        t.record_stream(side)
-
-
-def _returns_input(q, x) -> bool:
-    """Calling the TensorQuantizer ``q`` on ``x`` returns ``x`` itself (its side effects --
-    collecting, hooks -- do not change what the caller computes): the collect-only calibration
-    call, or a disabled quantizer, with no pre_quant_scale and no block reshape."""
-    return type(x) is torch.Tensor and isinstance(q, TensorQuantizer) and q.returns_input_unchanged()
+def _returns_input_q(q) -> bool:
+    """The TensorQuantizer ``q`` hands a plain tensor input back unchanged (collect-only
+    calibration or disabled, no pre_quant_scale, no block reshape; see
+    TensorQuantizer.returns_input_unchanged)."""
+    return isinstance(q, TensorQuantizer) and q.returns_input_unchanged()
 
 
 def _token_separable(q) -> bool:

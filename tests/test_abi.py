@@ -110,3 +110,17 @@ def test_attention_stride_preconditions_rejected_without_gpu():
     huge = list(dense)
     huge[4] = (1 << 31) // 128  # 64 tokens x 2 B x stride = 2^31 bytes
     assert call(huge) == -1
+
+
+def test_dispatch_registry_names_and_counts():
+    """mtq_dispatch_counts / mtq_dispatch_name (the tracing registry): every family named, counts
+    non-negative integers that never decrease (no GPU launch here, so they stay put)."""
+    from modelopt_amd import _ext
+
+    a = _ext.dispatch_counts()
+    assert len(a) >= 17 and all(k and isinstance(v, int) and v >= 0 for k, v in a.items())
+    assert {"ew_vec", "ew_group_sk", "ew_rowwave", "amax_persist", "awq_search_pp"} <= set(a)
+    lib = _ext.kernel_cdll()
+    assert lib.mtq_dispatch_counts(None, -1) == -1
+    assert lib.mtq_dispatch_name(len(a)) is None
+    assert _ext.dispatch_counts() == a
