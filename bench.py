@@ -172,11 +172,14 @@ def kernel_suite(ops, xs, steps, warmup):
     amax_t = torch.tensor(8.0, device="cuda")
     blk = [x.view(-1, BLOCK).abs().amax(dim=1, keepdim=True).float() for x in xs]
     rows = [x.abs().amax(dim=1, keepdim=True).float() for x in xs]
+    rows_own = [r.to(x.dtype) for r, x in zip(rows, xs)]  # what mtq stores for a bf16 model's weights
     cases = {
         "fp8_per_tensor": (lambda x: ops.fake_e4m3fy(x, amax_t), 4),
         "int8_per_tensor": (lambda x: ops.fake_tensor_quant(x, amax_t, 8, False, False), 4),
         "int8_per_channel_axis0": (
             lambda x: ops.quantize_op(x, rows[[id(t) for t in xs].index(id(x))], 8, 0, False, False), 4),
+        "int8_per_channel_axis0_bf16amax": (
+            lambda x: ops.quantize_op(x, rows_own[[id(t) for t in xs].index(id(x))], 8, 0, False, False), 4),
         "int4_block128_static": (
             lambda x: ops.quantize_op(x.view(-1, BLOCK), blk[[id(t) for t in xs].index(id(x))], 4, 0, False, False), 4),
         "mxfp4_block32_dynamic": (lambda x: ops.fused_amax_convert(x, 32, 6, 9, None), 4),
@@ -226,6 +229,7 @@ def kernel_suite(ops, xs, steps, warmup):
     nb = big[0].numel()
     for name, fn in {
         "histogram_2048_abs_117M_histc16": lambda x: _histc_counts(x, hmax, 2048, False, threads=16),
+        "histogram_2048_abs_117M_histc16_skip_zeros": lambda x: _histc_counts(x, hmax, 2048, True, threads=16),
         "histogram_2048_abs_117M_exact": lambda x: ops.histogram_abs_accumulate(x, hmax, counts, 2048, False) or counts,
     }.items():
         _, ms = time_kernel(fn, big, max(steps // 2, 5), min(warmup, 3))

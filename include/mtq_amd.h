@@ -172,16 +172,30 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
 /* torch.histc's CPU accumulation for calls above 2^24 elements (calib/histogram.py:116-130 ->
  * torch.histc -> at::parallel_for): element chunk c is [bounds[c], bounds[c+1]) (device int64
  * [chunks + 1], e.g. the skip_zeros boundaries mapped back to the input), or, with bounds null,
- * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  One launch: each chunk is counted exactly
- * into its row of `scratch` (uint32 [chunks * bins + 1]: the rows, then a block counter; ALL ZERO
- * on entry, left all zero on return -- keep one per stream and reuse it), and the launch's last
- * workgroup writes hist[b] = sum_c min(fp32(scratch[c][b]), 2^24) in chunk order (fp32 [bins],
- * overwritten).
+ * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  Two launches: each chunk is counted exactly
+ * into its row of `scratch` (uint32 [chunks * bins]: ALL ZERO on entry, left all zero on return --
+ * keep one per stream and reuse it), then hist[b] = sum_c min(fp32(scratch[c][b]), 2^24) in chunk
+ * order, + accum[b] for b < accum_n (the calibrator's running histogram, calib/histogram.py:127;
+ * accum may alias hist; accum_n 0 = none) (fp32 [bins], overwritten).
  * bf16 / f16 only, x 16-byte aligned, n % 8 == 0, bins <= 8192 (MTQ_ERR_DTYPE /
  * MTQ_ERR_INVALID_ARG otherwise: the caller counts chunk by chunk with mtq_histogram_abs). */
 int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                               int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
-                              uint32_t *scratch, float *hist, hipStream_t stream);
+                              uint32_t *scratch, const float *accum, int64_t accum_n, float *hist,
+                              hipStream_t stream);
+
+/* The skip_zeros chunk boundaries of the call above, computed on the device (no host sync):
+ * torch.histc counts the N non-zero elements as at::parallel_for chunks -- T' = min(threads,
+ * ceil(N / grain)), chunk = ceil(N / T'), chunk t = non-zero ranks [t * chunk, (t + 1) * chunk)
+ * (calib/histogram.py:116-130 -> torch.histc; grain = at::internal::GRAIN_SIZE = 32768) -- and
+ * bounds[t] (device int64 [threads + 1]) is the input index of chunk t's first element, n for an
+ * empty chunk: pass bounds and `threads` as chunks to mtq_histogram_abs_chunked.  workspace: int32
+ * [mtq_histogram_nonzero_bounds_workspace(n)] per-tile counts, contents irrelevant.  bf16 / f16, x
+ * 16-byte aligned, n % 8 == 0.  Zero = |x| bit pattern 0 (+0 and -0). */
+int64_t mtq_histogram_nonzero_bounds_workspace(int64_t n);
+int mtq_histogram_nonzero_bounds(const void *x, int64_t n, int dtype, int threads, int64_t grain,
+                                 int32_t *workspace, int64_t workspace_words, int64_t *bounds,
+                                 hipStream_t stream);
 
 /* ---- NVFP4 --------------------------------------------------------------------------------
  * Two-level dynamic NVFP4 fake quant of x [rows, cols] (blocks of block_size along cols, zero

@@ -60,7 +60,7 @@ def build_kernels(force: bool = False) -> Path:
             CSRC / "mtq_attention.hip", CSRC / "mtq_cpu.cpp"]
     hdrs = [CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
     OBJ.mkdir(parents=True, exist_ok=True)
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{INC}"]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror=misleading-indentation", "-Wno-unused-function", f"-I{INC}"]
     objs, jobs = [], []
     for src in srcs:
         obj = OBJ / (src.name + ".o")

@@ -418,7 +418,7 @@ enum DispatchId {
   kDispEwVec, kDispEwGroupSk, kDispEwGroup, kDispEwRowwave, kDispAmaxPersist, kDispAmaxRowsU,
   kDispAmaxRowsShort, kDispAmaxColsWide, kDispBlockQuantDyn, kDispHistValue, kDispHistValueChunked,
   kDispMxVec, kDispMxE2m1Native, kDispNvfp4NativeU, kDispAwqSearchPp, kDispAwqPrescale, kDispAwqMseMulti,
-  kDispCount
+  kDispHistNzBounds, kDispCount
 };
 void count_dispatch(int id);
 

@@ -394,10 +394,12 @@ __global__ __launch_bounds__(kThreads) void ew_group_sk_kernel(const T *__restri
 // per-vector channel division, per-lane amax load and per-vector scale computation of the
 // element-wise kernel disappear.  Lane l of the wave takes vectors wb + l + 64 u (each load
 // instruction covers 1 KiB contiguous).  Requires axis_size * vb == nvec (no outer wrap).
-template <typename T, class Op, int U>
+// A: the amax storage type -- fp32, or the input's own 16-bit type (a bf16 model's per-channel
+// weight amax is bf16, reference tensor_quantizer.py `_get_amax` keeps the input dtype).
+template <typename T, typename A, class Op, int U>
 __global__ __launch_bounds__(kThreads) void ew_rowwave_kernel(const T *__restrict__ x,
                                                                T *__restrict__ y, int64_t nvec,
-                                                               const float *__restrict__ amax,
+                                                               const A *__restrict__ amax,
                                                                int64_t vb, Op op) {
   using V = Vec<T>;
   const int lane = threadIdx.x & 63;
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(kThreads) void ew_rowwave_kernel(const T *__restric
   }
   if (wb >= nvec) return;
   const int64_t c = wb / vb;  // wave-uniform (scalar)
-  const auto q = op.qparam_from(amax[c]);
+  const auto q = op.qparam_from((float)amax[c]);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = wb + u * 64 + lane;
@@ -465,10 +467,11 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
           go(std::integral_constant<int, 16>{});
         else
           go(std::integral_constant<int, 32>{});
-      } else if (nvec > 0)
+      } else if (nvec > 0) {
         count_dispatch(kDispEwGroup);
         ew_group_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
             reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec, (int)(vb / U), op);
+      }
       const int64_t done = nvec * N;
       if (done < n) {
         unsigned gs = grid_for(n - done, kThreads);
@@ -479,16 +482,24 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
     }
     // long channels (per-row weights): channel length a multiple of 128 vectors, fp32 amax,
     // 16-byte aligned, no outer wrap -> wave-uniform channel
+    const bool amax_own = (op.amax_dtype == MTQ_BF16 && __is_same(T, __bf16)) ||
+                          (op.amax_dtype == MTQ_F16 && __is_same(T, _Float16));
     if (vb >= 128 && vb % 128 == 0 && aligned16(x) && aligned16(y) &&
-        op.amax_dtype == MTQ_F32 && axis_size * vb == n / N && n % N == 0) {
+        (op.amax_dtype == MTQ_F32 || amax_own) && axis_size * vb == n / N && n % N == 0) {
       constexpr int U = 2;
       const int64_t nvec = n / N;
       const unsigned g = (unsigned)((nvec + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U));
-      if (nvec > 0)
+      if (nvec > 0) {
         count_dispatch(kDispEwRowwave);
-        ew_rowwave_kernel<T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
-            reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
-            reinterpret_cast<const float *>(op.amax), vb, op);
+        if (op.amax_dtype == MTQ_F32)
+          ew_rowwave_kernel<T, float, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
+              reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
+              reinterpret_cast<const float *>(op.amax), vb, op);
+        else
+          ew_rowwave_kernel<T, T, VecOp<T>, U><<<g, kThreads, 0, stream>>>(
+              reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
+              reinterpret_cast<const T *>(op.amax), vb, op);
+      }
       return check_launch();
     }
     return launch_ew<T>(x, y, n, op, stream);
@@ -1321,20 +1332,43 @@ constexpr int kHistPatterns = 32768;
 // blocks and the count row counts[c * bins, +bins); element bounds need not fall on vectors, so
 // the two edge vectors of a chunk mask their out-of-chunk halves to the dropped NaN pattern.
 //
-// The launch also finishes the job (one launch per call): every block adds its bins into its
-// chunk's row with device-scope atomics, and the last block to finish (agent-scope counter in
-// the scratch's last word) folds hist[b] = sum_c min(fp32(row_c[b]), 2^24) in chunk order, then
-// zeroes the rows and the counter again -- the scratch is all zero between calls, so no memset
-// and no second launch is needed.
+// The rows are folded by a second, small launch (hist_fold_rows_kernel): hist[b] = sum_c
+// min(fp32(row_c[b]), 2^24) in chunk order (+ an optional running histogram), zeroing the rows
+// again -- the scratch is all zero between calls, so no memset is needed.  (r05: the fold in the
+// counting launch -- each workgroup waiting for its row atomics, an agent-scope check-in counter,
+// the last workgroup exchanging 32 K words -- cost 12 us at the launch's tail against 5.5 us for
+// the second launch; bf16 [8192, 14336], 16 chunks, 2048 bins.)
 struct HistChunks {
   const int64_t *bounds;  // [chunks + 1] element offsets (device), or null: uniform chunks
   int64_t chunk_elems;
   int64_t n_elems;
   int bpc;  // blocks per chunk
   int chunks;
-  uint32_t *rows;  // [chunks, bins] counts, then the block counter; zero on entry and on exit
-  float *hist;     // [bins] fp32 result
+  uint32_t *rows;  // [chunks, bins] counts; zero on entry, zeroed again by the fold launch
 };
+
+// hist[b] = sum_c min(fp32(rows[c][b]), 2^24) in chunk order (torch.histc's thread-order fold of
+// its fp32 per-thread counts), then + accum[b] for b < accum_n (the calibrator's running
+// histogram, `hist[:old.numel()] += old`), rows zeroed.  16 chunks' loads in flight per lane.
+__global__ __launch_bounds__(256) void hist_fold_rows_kernel(uint32_t *__restrict__ rows, int chunks, int bins,
+                                                             const float *accum, int64_t accum_n,
+                                                             float *hist) {  // accum may alias hist
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= bins) return;
+  float h = 0.f;
+  for (int c0 = 0; c0 < chunks; c0 += 16) {
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = c0 + j < chunks ? rows[(int64_t)(c0 + j) * bins + b] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      h += fminf((float)v[j], 16777216.f);  // + 0 past the last chunk
+      if (c0 + j < chunks) rows[(int64_t)(c0 + j) * bins + b] = 0u;
+    }
+  }
+  if (b < accum_n) h += accum[b];
+  hist[b] = h;
+}
 
 template <typename T, int U, bool PF, bool CHUNKED = false>
 __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
@@ -1383,11 +1417,15 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
       e1 = e0 + ch.chunk_elems;
       e1 = e1 < ch.n_elems ? e1 : ch.n_elems;
     }
-    const int64_t cv0 = e0 / 8, cv1 = (e1 + 7) / 8;
+    // whole vectors inside [e0, e1) go through the hot loop unmasked; the (at most two) vectors a
+    // chunk edge cuts are counted below by lane 0 of the chunk's first block (masking them at load
+    // time made every prefetch wait for its data: 53 vs 41 us, r05d)
+    const int64_t cv0 = (e0 + 7) / 8, cv1 = e1 / 8 > cv0 ? e1 / 8 : cv0;
     const int64_t per = (cv1 - cv0 + ch.bpc - 1) / ch.bpc;
     v0 = cv0 + (int64_t)s * per;
     v1 = v0 + per;
     v1 = v1 < cv1 ? v1 : cv1;
+    v0 = v0 < v1 ? v0 : v1;
     counts += (int64_t)c * bins;
   } else {
     v0 = (int64_t)blockIdx.x * vec_per_block;
@@ -1403,17 +1441,6 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
       if (k < v1) {
         const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + k * 8));
         v[u] = make_uint4(r.x, r.y, r.z, r.w);
-        if constexpr (CHUNKED) {
-          if (k * 8 < e0 || k * 8 + 8 > e1) {  // a chunk's edge vector: drop the outside halves
-            uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int64_t e = k * 8 + j;
-              if (e < e0 || e >= e1) w[j / 2] |= 0x7FFFu << (16 * (j % 2));
-            }
-            v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-          }
-        }
       } else {
         v[u] = make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
       }
@@ -1449,6 +1476,22 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
       uint4 v[U];
       load(i, v);
       count(v);
+    }
+  }
+  if constexpr (CHUNKED) {
+    if (blockIdx.x % ch.bpc == 0 && threadIdx.x == 0 && e1 > e0) {
+      // the chunk's cut edge vectors: the head one holding e0 (when e0 is not vector-aligned) and
+      // the tail one holding e1 - 1 (when e1 is not, and it is another vector); their halves
+      // outside [e0, e1) belong to the neighbouring chunks
+      const int64_t hv = e0 / 8, tv = (e1 - 1) / 8;
+      for (int64_t vv = hv; vv <= tv; vv += (tv > hv ? tv - hv : 1)) {
+        if (vv * 8 >= e0 && vv * 8 + 8 <= e1) continue;  // a whole vector: the hot loop had it
+        const uint16_t *h = reinterpret_cast<const uint16_t *>(x + vv * 8);
+        for (int j = 0; j < 8; ++j) {
+          const int64_t e = vv * 8 + j;
+          if (e >= e0 && e < e1) atomicAdd(vh + (h[j] & 0x7FFFu), 1u);
+        }
+      }
     }
   }
   __syncthreads();
@@ -1491,33 +1534,131 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   __syncthreads();
   for (int b = threadIdx.x; b < bins; b += kHistValThreads)
     if (bh[b]) atomicAdd(counts + b, bh[b]);
-  if constexpr (CHUNKED) {
-    // (the flag lives in the dynamic LDS, free again here: a static __shared__ variable would
-    // push static + dynamic LDS past the 160 KiB the launch reserves)
-    // this wave's row atomics performed (workgroup-scope release: a vscnt / vmcnt wait, no L2
-    // writeback -- a device-scope fence in every lane cost more than the whole count), then one
-    // device-scope acq_rel check-in per block
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    uint32_t *counter = ch.rows + (int64_t)ch.chunks * bins;
-    if (threadIdx.x == 0) {
-      const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      sh[0] = done == gridDim.x - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!sh[0]) return;
-    // the rows are read and cleared with device-scope atomic loads / stores (past the caches)
-    for (int b = threadIdx.x; b < bins; b += kHistValThreads) {
-      float h = 0.f;
-      for (int c = 0; c < ch.chunks; ++c) {
-        uint32_t *r = ch.rows + (int64_t)c * bins + b;
-        const uint32_t v = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        h += fminf((float)v, 16777216.f);
-        __hip_atomic_store(r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// skip_zeros chunk boundaries on the device (replaces an int64 cumsum over the whole input, a
+// host sync on its last element and a searchsorted; r05b: 1.25 ms for bf16 [8192, 14336]).
+// torch.histc counts the compacted non-zero elements, N of them, as at::parallel_for chunks:
+// T' = min(T, ceil(N / grain)) threads, chunk = ceil(N / T'), chunk t = compacted ranks
+// [t * chunk, (t + 1) * chunk).  Its first element in the input is bounds[t]; chunks at or past
+// N are empty (bounds = n).
+//   1. hist_nz_tiles_kernel: non-zero |x| count per tile of kNzTileVec vectors (one read of x);
+//   2. hist_nz_bounds_kernel: block t sums the tile counts (N), finds the tile holding rank
+//      t * chunk by a block scan of the tile counts, then the element by a block scan of that
+//      tile's per-lane counts -- T + 1 blocks, ~2 tiles' reads in total.
+constexpr int kNzThreads = 1024;
+constexpr int kNzPerLane = 8;                            // vectors per lane
+constexpr int64_t kNzTileVec = (int64_t)kNzThreads * kNzPerLane;  // 8192 vectors = 65536 elements
+
+__device__ __forceinline__ int nz_halves(uint32_t w) {
+  return ((w & 0x7FFFu) != 0u) + ((w & 0x7FFF0000u) != 0u);
+}
+
+__device__ __forceinline__ int nz_vec(const u32x4 &v) {
+  return nz_halves(v.x) + nz_halves(v.y) + nz_halves(v.z) + nz_halves(v.w);
+}
+
+// exclusive prefix sum over the block (kNzThreads lanes); *total = the block's sum
+__device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t *sh_w, int64_t *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) sh_w[w] = inc;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+  for (int k = 0; k < kNzThreads / 64; ++k) {
+    base += k < w ? sh_w[k] : 0;
+    tot += sh_w[k];
+  }
+  __syncthreads();  // sh_w reusable
+  *total = tot;
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(kNzThreads) void hist_nz_tiles_kernel(const u32x4 *__restrict__ x, int64_t nvec,
+                                                                   int32_t *__restrict__ tiles) {
+  const int64_t t0 = (int64_t)blockIdx.x * kNzTileVec;
+  int c = 0;
+#pragma unroll
+  for (int u = 0; u < kNzPerLane; ++u) {
+    const int64_t i = t0 + (int64_t)u * kNzThreads + threadIdx.x;
+    if (i < nvec) c += nz_vec(__builtin_nontemporal_load(x + i));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ int sw[kNzThreads / 64];
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < kNzThreads / 64; ++k) t += sw[k];
+    tiles[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kNzThreads) void hist_nz_bounds_kernel(const u32x4 *__restrict__ x, int64_t nvec,
+                                                                    const int32_t *__restrict__ tiles,
+                                                                    int64_t ntiles, int threads, int64_t grain,
+                                                                    int64_t *__restrict__ bounds) {
+  __shared__ int64_t sh_w[kNzThreads / 64];
+  __shared__ int64_t sh_tile, sh_rem;
+  const int t = blockIdx.x;
+  const int64_t n = nvec * 8;
+  // tile counts: lane l owns the contiguous slice [l * per, (l + 1) * per)
+  const int64_t per = (ntiles + kNzThreads - 1) / kNzThreads;
+  const int64_t s0 = (int64_t)threadIdx.x * per;
+  int64_t mine = 0;
+  for (int64_t k = s0; k < s0 + per && k < ntiles; ++k) mine += tiles[k];
+  int64_t kept;
+  const int64_t before = block_exscan(mine, sh_w, &kept);
+  const int64_t tq = (kept + grain - 1) / grain;
+  const int64_t teff = (int64_t)threads < tq ? (int64_t)threads : tq;  // 0 when kept == 0
+  const int64_t chunk = teff > 0 ? (kept + teff - 1) / teff : 1;
+  const int64_t target = (int64_t)t * chunk;  // compacted rank of chunk t's first element
+  if (t == 0 || target >= kept) {
+    if (threadIdx.x == 0) bounds[t] = t == 0 ? 0 : n;
+    return;  // block-uniform
+  }
+  if (threadIdx.x == 0) sh_tile = -1;
+  __syncthreads();
+  if (before <= target && target < before + mine) {  // exactly one lane
+    int64_t acc = before, k = s0;
+    while (acc + tiles[k] <= target) acc += tiles[k++];
+    sh_tile = k;
+    sh_rem = target - acc;
+  }
+  __syncthreads();
+  const int64_t tile = sh_tile, rem = sh_rem;
+  // the tile's vectors: lane l owns [v0 + l * 8, + 8) (contiguous, so ranks follow lane order)
+  const int64_t v0 = tile * kNzTileVec + (int64_t)threadIdx.x * kNzPerLane;
+  u32x4 v[kNzPerLane];
+  int c = 0;
+#pragma unroll
+  for (int u = 0; u < kNzPerLane; ++u) {
+    v[u] = v0 + u < nvec ? x[v0 + u] : u32x4{0u, 0u, 0u, 0u};
+    c += nz_vec(v[u]);
+  }
+  int64_t tot;
+  const int64_t lb = block_exscan(c, sh_w, &tot);
+  if (lb <= rem && rem < lb + c) {  // exactly one lane holds the rem-th non-zero of the tile
+    int64_t r = rem - lb;
+#pragma unroll
+    for (int u = 0; u < kNzPerLane; ++u) {
+      const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const bool nz = (w4[h / 2] >> (16 * (h % 2)) & 0x7FFFu) != 0u;
+        if (nz) {
+          if (r == 0) bounds[t] = (v0 + u) * 8 + h;
+          --r;
+        }
       }
-      ch.hist[b] = h;
     }
-    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2601,7 +2742,7 @@ void count_dispatch(int id) { g_dispatch[id].fetch_add(1, std::memory_order_rela
 static const char *const kDispatchNames[kDispCount] = {
     "ew_vec", "ew_group_sk", "ew_group", "ew_rowwave", "amax_persist", "amax_rows_u", "amax_rows_short",
     "amax_cols_wide", "block_quant_dyn", "hist_value", "hist_value_chunked", "mx_vec", "mx_e2m1_native",
-    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi"};
+    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_nz_bounds"};
 }  // namespace mtq
 
 // ============================================================================================
@@ -2883,9 +3024,11 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
 
 int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                               int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
-                              uint32_t *scratch, float *hist, hipStream_t stream) {
+                              uint32_t *scratch, const float *accum, int64_t accum_n, float *hist,
+                              hipStream_t stream) {
   if (n < 0 || bins < 1 || bins > 8192 || chunks < 1 || !hmax || !scratch || !hist || (n > 0 && !x))
     return MTQ_ERR_INVALID_ARG;
+  if (accum_n < 0 || accum_n > bins || (accum_n > 0 && !accum)) return MTQ_ERR_INVALID_ARG;
   if (!bounds && (chunk_elems < 1 || (chunks - 1) * chunk_elems >= n)) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
   if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
@@ -2907,14 +3050,38 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
       }
-      const HistChunks ch{bounds, chunk_elems, n, (int)bpc, chunks, scratch, hist};
+      const HistChunks ch{bounds, chunk_elems, n, (int)bpc, chunks, scratch};
       count_dispatch(kDispHistValueChunked);
       kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
                                                                       hmax, bins, skip_zeros, scratch, ch);
+      hist_fold_rows_kernel<<<(unsigned)((bins + 255) / 256), 256, 0, stream>>>(scratch, chunks, bins, accum,
+                                                                                accum_n, hist);
       return check_launch();
     }
     return MTQ_ERR_DTYPE;
   });
+}
+
+int64_t mtq_histogram_nonzero_bounds_workspace(int64_t n) {
+  if (n < 0) return -1;
+  return (n / 8 + kNzTileVec - 1) / kNzTileVec;
+}
+
+int mtq_histogram_nonzero_bounds(const void *x, int64_t n, int dtype, int threads, int64_t grain,
+                                 int32_t *workspace, int64_t workspace_words, int64_t *bounds,
+                                 hipStream_t stream) {
+  if (n < 0 || threads < 1 || grain < 1 || !bounds || (n > 0 && (!x || !workspace))) return MTQ_ERR_INVALID_ARG;
+  if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
+  if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
+  const int64_t nvec = n / 8, ntiles = mtq_histogram_nonzero_bounds_workspace(n);
+  if (workspace_words < ntiles) return MTQ_ERR_INVALID_ARG;
+  if (ntiles > 0)
+    hist_nz_tiles_kernel<<<(unsigned)ntiles, kNzThreads, 0, stream>>>(reinterpret_cast<const u32x4 *>(x), nvec,
+                                                                      workspace);
+  count_dispatch(kDispHistNzBounds);
+  hist_nz_bounds_kernel<<<(unsigned)(threads + 1), kNzThreads, 0, stream>>>(
+      reinterpret_cast<const u32x4 *>(x), nvec, workspace, ntiles, threads, grain, bounds);
+  return check_launch();
 }
 
 int64_t mtq_mse_workspace_floats(int64_t n, int dtype) {

@@ -923,7 +923,8 @@ void histogram_abs_accumulate(const at::Tensor &inputs, const at::Tensor &hmax, 
 at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hmax, int64_t bins,
                                  bool skip_zeros, const c10::optional<at::Tensor> &bounds,
                                  int64_t chunk_elems, int64_t chunks,
-                                 const c10::optional<at::Tensor> &scratch_in) {
+                                 const c10::optional<at::Tensor> &scratch_in,
+                                 const c10::optional<at::Tensor> &accum_in) {
   at::Tensor x = inputs.contiguous();
   check_device(x, "inputs");
   TORCH_CHECK(hmax.scalar_type() == at::kFloat && hmax.numel() == 1, "histogram: hmax fp32 scalar");
@@ -943,19 +944,49 @@ at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hma
   if (scratch_in.has_value() && scratch_in->defined()) {
     scratch = *scratch_in;
     TORCH_CHECK(scratch.scalar_type() == at::kInt && scratch.is_contiguous() && scratch.device() == x.device() &&
-                    scratch.numel() >= chunks * bins + 1,
-                "histogram_abs_chunked: scratch must be contiguous int32 [>= chunks * bins + 1] on the input's device");
+                    scratch.numel() >= chunks * bins,
+                "histogram_abs_chunked: scratch must be contiguous int32 [>= chunks * bins] on the input's device");
   } else {
-    scratch = at::zeros({chunks * bins + 1}, x.options().dtype(at::kInt));
+    scratch = at::zeros({chunks * bins}, x.options().dtype(at::kInt));
+  }
+  // accum: a running fp32 histogram added into the result (its first accum.numel() bins)
+  at::Tensor accum;
+  if (accum_in.has_value() && accum_in->defined()) {
+    accum = accum_in->contiguous();
+    TORCH_CHECK(accum.scalar_type() == at::kFloat && accum.dim() == 1 && accum.numel() <= bins &&
+                    accum.device() == x.device(),
+                "histogram_abs_chunked: accum must be fp32 [<= bins] on the input's device");
   }
   at::Tensor hist = at::empty({bins}, x.options().dtype(at::kFloat));
   int st = mtq_histogram_abs_chunked(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"),
                                      hmax.data_ptr<float>(), (int)bins, skip_zeros ? 1 : 0, bp,
                                      chunk_elems, (int)chunks,
                                      reinterpret_cast<uint32_t *>(scratch.data_ptr<int32_t>()),
-                                     hist.data_ptr<float>(), cur_stream(x));
+                                     accum.defined() ? accum.data_ptr<float>() : nullptr,
+                                     accum.defined() ? accum.numel() : 0, hist.data_ptr<float>(),
+                                     cur_stream(x));
   check_status(st, "histogram_abs_chunked");
   return hist;
+}
+
+// torch.histc's chunking with skip_zeros, all on the device: the non-zero chunk boundaries
+// (mtq_histogram_nonzero_bounds), then the one-launch chunked count over them
+at::Tensor histogram_abs_chunked_nonzero(const at::Tensor &inputs, const at::Tensor &hmax, int64_t bins,
+                                         int64_t threads, const c10::optional<at::Tensor> &scratch_in,
+                                         const c10::optional<at::Tensor> &accum) {
+  at::Tensor x = inputs.contiguous();
+  check_device(x, "inputs");
+  TORCH_CHECK(threads >= 1 && threads <= (1 << 20), "histogram_abs_chunked_nonzero: bad thread count");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t ws = mtq_histogram_nonzero_bounds_workspace(x.numel());
+  TORCH_CHECK(ws >= 0, "histogram_abs_chunked_nonzero: bad size");
+  at::Tensor tiles = at::empty({ws > 0 ? ws : 1}, x.options().dtype(at::kInt));
+  at::Tensor bounds = at::empty({threads + 1}, x.options().dtype(at::kLong));
+  int st = mtq_histogram_nonzero_bounds(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"), (int)threads,
+                                        32768, tiles.data_ptr<int32_t>(), ws, bounds.data_ptr<int64_t>(),
+                                        cur_stream(x));
+  check_status(st, "histogram_nonzero_bounds");
+  return histogram_abs_chunked(x, hmax, bins, true, bounds, 0, threads, scratch_in, accum);
 }
 
 // ---- reference torch.library ops (tensor_quant.py:115-195) -------------------------------------
@@ -1093,7 +1124,9 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("histogram_abs_accumulate(Tensor inputs, Tensor hmax, Tensor(a!) counts, int bins, "
         "bool skip_zeros) -> ()");
   m.def("histogram_abs_chunked(Tensor inputs, Tensor hmax, int bins, bool skip_zeros, Tensor? bounds, "
-        "int chunk_elems, int chunks, Tensor(a!)? scratch=None) -> Tensor");
+        "int chunk_elems, int chunks, Tensor(a!)? scratch=None, Tensor? accum=None) -> Tensor");
+  m.def("histogram_abs_chunked_nonzero(Tensor inputs, Tensor hmax, int bins, int threads, "
+        "Tensor(a!)? scratch=None, Tensor? accum=None) -> Tensor");
   m.def("qlinear_small_m_group(Tensor[] inputs, Tensor[] weights, Tensor?[] biases, Tensor[] amaxs, int[] blocks, "
         "int kind, int[] num_bits, int[] is_unsigned, int[] narrow_range) -> Tensor[]");
   m.def("qlinear_small_m(Tensor input, Tensor weight, Tensor? bias, Tensor amax, int block, int kind, "
@@ -1143,6 +1176,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("block_quant_dynamic", &block_quant_dynamic);
   m.impl("histogram_abs_accumulate", &histogram_abs_accumulate);
   m.impl("histogram_abs_chunked", &histogram_abs_chunked);
+  m.impl("histogram_abs_chunked_nonzero", &histogram_abs_chunked_nonzero);
   m.impl("mse_accumulate", &mse_accumulate);
   m.impl("mul_cols", &mul_cols);
   m.impl("awq_search_gemm", &awq_search_gemm);

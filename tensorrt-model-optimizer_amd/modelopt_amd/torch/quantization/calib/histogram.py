@@ -96,10 +96,10 @@ class HistogramCalibrator(_Calibrator):
             bins = self._num_bins
             hmax = self._calib_bin_edges[-1].to(device=x.device, dtype=torch.float32).reshape(())
             old = self._calib_hist
-        hist = _histc_counts(x, hmax.float().contiguous(), bins, self._skip_zeros, self._histc_threads)
         if old is not None:
-            hist[: old.numel()] += old.to(hist.device)
-        self._calib_hist = hist
+            old = old.to(x.device)
+        self._calib_hist = _histc_counts(x, hmax.float().contiguous(), bins, self._skip_zeros,
+                                         self._histc_threads, accum=old)
 
     def reset(self):
         self._calib_bin_edges = None
@@ -152,7 +152,7 @@ def _chunk_scratch(device: torch.device, words: int) -> torch.Tensor:
     key = (device, torch.cuda.current_stream(device).cuda_stream)
     buf = _CHUNK_SCRATCH.get(key)
     if buf is None or buf.numel() < words:
-        buf = _CHUNK_SCRATCH[key] = torch.zeros(max(words, 16 * 8192 + 1), dtype=torch.int32, device=device)
+        buf = _CHUNK_SCRATCH[key] = torch.zeros(max(words, 16 * 8192), dtype=torch.int32, device=device)
     return buf
 
 
@@ -162,22 +162,45 @@ def _histc_threads() -> int:
 
 
 def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bool,
-                  threads: int | None = None) -> torch.Tensor:
+                  threads: int | None = None, accum: torch.Tensor | None = None) -> torch.Tensor:
     """fp32 per-call histogram of |x| over [0, hmax] with torch.histc's CPU accumulation.
 
     Every count of a call with at most 2^24 (kept) elements is exact in fp32 whatever the chunking,
     so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T = threads``,
     default ``_histc_threads()``; chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted
     exactly, clamped at 2^24 and added into the fp32 result in thread order: bf16 / f16 on the GPU
-    in one launch for all chunks (histogram_abs_chunked), other inputs one launch per chunk."""
+    in one launch for all chunks (histogram_abs_chunked; with ``skip_zeros`` the non-zero chunk
+    boundaries are found on the device first, histogram_abs_chunked_nonzero), other inputs one
+    launch per chunk.  ``accum`` (the calibrator's running histogram, ``numel <= bins``) is added
+    into the first bins of the result (``hist[:old.numel()] += old``, reference histogram.py:127),
+    in the chunk fold's launch on the one-launch path."""
+
+    def plus_accum(hist):
+        if accum is not None:
+            hist[: accum.numel()] += accum
+        return hist
+
     ops = _ops()
     n = x.numel()
     mode = os.environ.get("MTQ_AMD_HIST_COUNTS", "histc")
     if n <= _F32_COUNT_LIMIT or mode == "exact":
         counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
         ops.histogram_abs_accumulate(x, hmax, counts, bins, skip_zeros)
-        return counts.float()
+        return plus_accum(counts.float())
     flat = x.contiguous().reshape(-1)
+    gpu_one_launch = (flat.is_cuda and flat.dtype in (torch.bfloat16, torch.float16) and bins <= 8192
+                      and n % 8 == 0 and flat.data_ptr() % 16 == 0)
+    if skip_zeros and gpu_one_launch:
+        # the non-zero chunk boundaries found on the device (per-tile non-zero counts, then one
+        # block per boundary), no host sync; with at most 2^24 non-zeros every count is exact in
+        # fp32, so the chunked sum equals the single-launch count there too
+        t = threads or _histc_threads()
+        scratch = _chunk_scratch(flat.device, t * bins)
+        try:
+            return ops.histogram_abs_chunked_nonzero(flat, hmax, bins, t, scratch, accum)
+        except Exception:
+            _CHUNK_SCRATCH.clear()
+            raise
     if skip_zeros:
         # chunk boundaries live in the compacted (non-zero) index space: map them back
         csum = torch.cumsum((flat != 0).to(torch.int64), 0)
@@ -187,7 +210,7 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     if kept <= _F32_COUNT_LIMIT:
         counts = torch.zeros(bins, dtype=torch.int32, device=x.device)
         ops.histogram_abs_accumulate(flat, hmax, counts, bins, skip_zeros)
-        return counts.float()
+        return plus_accum(counts.float())
     threads = min(threads or _histc_threads(), -(-kept // _HISTC_GRAIN))
     chunk = -(-kept // threads)
     starts = [t * chunk for t in range(threads) if t * chunk < kept] + [kept]
@@ -195,17 +218,12 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     if csum is not None:
         # the first original index whose non-zero rank reaches each compacted start
         cuts = torch.searchsorted(csum, torch.tensor(starts[1:-1], device=csum.device, dtype=torch.int64) + 1)
-    if (flat.is_cuda and flat.dtype in (torch.bfloat16, torch.float16) and bins <= 8192 and n % 8 == 0
-            and flat.data_ptr() % 16 == 0):
+    if gpu_one_launch:
         # one launch counts every chunk into its own row; its last workgroup adds the clamped rows in order
         nch = len(starts) - 1
-        dev_bounds = None
-        if cuts is not None:
-            z = torch.zeros(1, dtype=torch.int64, device=flat.device)
-            dev_bounds = torch.cat([z, cuts, torch.full_like(z, n)])
-        scratch = _chunk_scratch(flat.device, nch * bins + 1)
+        scratch = _chunk_scratch(flat.device, nch * bins)
         try:
-            return ops.histogram_abs_chunked(flat, hmax, bins, skip_zeros, dev_bounds, chunk, nch, scratch)
+            return ops.histogram_abs_chunked(flat, hmax, bins, False, None, chunk, nch, scratch, accum)
         except Exception:
             _CHUNK_SCRATCH.clear()  # a failed launch may leave it non-zero
             raise
@@ -217,7 +235,7 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
         if e > b:
             ops.histogram_abs_accumulate(flat[b:e], hmax, counts, bins, skip_zeros)
         hist += counts.float().clamp_(max=_F32_COUNT_LIMIT)
-    return hist
+    return plus_accum(hist)
 
 
 def _compute_amax_entropy(calib_hist, calib_bin_edges, num_bits, unsigned, stride=1, start_bin=128):

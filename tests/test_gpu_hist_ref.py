@@ -186,3 +186,78 @@ def test_histc_chunked_scratch_left_zero_and_reusable(gpu):
             got = ops.histogram_abs_chunked(x, hmax, bins, False, None, chunk, chunks, scratch)
             assert torch.equal(got, fresh), (chunks, bins)
             assert int(scratch.abs().sum()) == 0, "scratch not left zero"
+
+
+def _host_nonzero_bounds(x, threads, grain=32768):
+    """torch.histc's skip_zeros chunking restated on the host: T' = min(T, ceil(N / grain)),
+    chunk = ceil(N / T'), chunk t starts at the input index of the (t * chunk)-th non-zero."""
+    nz = torch.nonzero(x.view(-1).float() != 0).view(-1).cpu()
+    kept, n = nz.numel(), x.numel()
+    teff = min(threads, -(-kept // grain))
+    chunk = -(-kept // teff) if teff else 1
+    return [0] + [int(nz[t * chunk]) if t * chunk < kept else n for t in range(1, threads)] + [n]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_histc_nonzero_bounds_on_device(gpu, dtype):
+    """skip_zeros chunking found on the device (histogram_abs_chunked_nonzero: per-tile non-zero
+    counts, one block per boundary) against host-computed bounds fed to histogram_abs_chunked:
+    scattered and clustered zeros, a zero-free and an all-zero input, -0, NaN (kept, as x != 0
+    keeps it), T = 1, T past ceil(N / grain), a chunk boundary inside a vector."""
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    g = torch.Generator(device=gpu).manual_seed(9)
+    hmax = torch.tensor([6.0], device=gpu)
+    n = 8 * 1_300_007
+    base = (torch.randn(n, device=gpu, generator=g) * 2).to(dtype)
+    cases = {}
+    x = base.clone()
+    x[::3] = 0
+    x[5::7] = -0.0
+    cases["scattered"] = x
+    x = base.clone()
+    x[: n // 3] = 0  # the first chunks' boundaries all fall in one zero run
+    x[n // 2: n // 2 + 70_001] = 0
+    x[123] = float("nan")
+    cases["clustered"] = x
+    cases["no_zeros"] = base.abs() + 0.01
+    cases["all_zero"] = torch.zeros(n, dtype=dtype, device=gpu)
+    x = torch.zeros(n, dtype=dtype, device=gpu)
+    x[1000:1000 + 40_000] = 1.0  # N = 40000: T' = 2 of T = 16
+    cases["few_nonzeros"] = x
+    for name, x in cases.items():
+        for threads in (1, 3, 16, 700):
+            want_b = _host_nonzero_bounds(x, threads)
+            want = ops.histogram_abs_chunked(x, hmax, 2048, True,
+                                             torch.tensor(want_b, dtype=torch.int64, device=gpu), 0, threads)
+            got = ops.histogram_abs_chunked_nonzero(x, hmax, 2048, threads)
+            assert torch.equal(got, want), (name, threads)
+
+
+def test_histc_skip_zeros_above_2p24_no_host_sync(gpu):
+    """The calibrator's > 2^24 skip_zeros call issues no device -> host copy (the device-side
+    bounds replace cumsum + int(csum[-1]) + searchsorted) and equals the per-chunk count over the
+    host-computed bounds; with at most 2^24 non-zeros it equals the exact single launch."""
+    from modelopt_amd import _ext
+    from modelopt_amd.torch.quantization.calib.histogram import _histc_counts
+
+    ops = _ext.ops()
+    n = 2**24 + 8 * 4099
+    g = torch.Generator(device=gpu).manual_seed(4)
+    x = (torch.randn(n, device=gpu, generator=g)).to(torch.bfloat16)
+    x[::4] = 0
+    x[1::9] = 0.5
+    hmax = torch.tensor([5.0], device=gpu)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        got = _histc_counts(x, hmax, 2048, True, threads=16)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    b = _host_nonzero_bounds(x, 16)
+    want = ops.histogram_abs_chunked(x, hmax, 2048, True, torch.tensor(b, dtype=torch.int64, device=gpu), 0, 16)
+    assert torch.equal(got, want)
+    exact = torch.zeros(2048, dtype=torch.int32, device=gpu)
+    ops.histogram_abs_accumulate(x, hmax, exact, 2048, True)
+    assert torch.equal(got, exact.float())  # 0.75 n non-zeros < 2^24: every count exact

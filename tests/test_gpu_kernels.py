@@ -161,6 +161,29 @@ def test_int_bf16_amax_dtype(gpu):
     assert same_bits(out, ref), mismatch(out, ref)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("fmt", ["int8", "int4", "fp8"])
+@pytest.mark.parametrize("shape", [(16, 2048), (6, 1024), (96, 4096)])
+def test_long_rows_own_dtype_amax(gpu, dtype, fmt, shape):
+    """A bf16 / f16 model's per-channel weight amax is kept in the weight's dtype (MaxCalibrator):
+    the wave-uniform row kernel reads it in that dtype (mtq_dispatch_counts shows ew_rowwave)."""
+    from modelopt_amd import _ext
+
+    x = rand_with_edges(shape, dtype, seed=21)
+    amax = x.abs().amax(dim=1, keepdim=True)
+    amax.view(-1)[1] = 0.0
+    before = _ext.dispatch_counts()["ew_rowwave"]
+    if fmt == "fp8":
+        ref = R.fp8_eager(x, amax)
+        out = ops().quantize_op(x.to(gpu), amax.to(gpu), 8, 4, False, False)
+    else:
+        bits = 8 if fmt == "int8" else 4
+        ref = R.tensor_quant(x, amax, bits, False, False)
+        out = ops().quantize_op(x.to(gpu), amax.to(gpu), bits, 0, False, False)
+    assert same_bits(out, ref), mismatch(out, ref)
+    assert _ext.dispatch_counts()["ew_rowwave"] == before + 1
+
+
 # --------------------------------------------------------------------------------------------
 # FP8
 # --------------------------------------------------------------------------------------------

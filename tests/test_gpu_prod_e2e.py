@@ -23,8 +23,10 @@ reference run's sha256 fingerprint first.  Criteria:
   summed in another order over activations that differ as above), best scales rtol 2e-2 where the
   alpha agrees; the static-block weight amax bit-equal count is reported (a 1-ulp act_scale
   difference changes the scale and so the block amax);
-* logits: max error below 10 % of the largest logit and cosine above 0.999 (a 1-ulp amax
-  difference moves an FP8 scale).
+* logits: against a noise floor measured in the test -- the same GPU forward with the reference
+  run's amax loaded into the quantizers.  The remaining distance is the GPU-vs-CPU bf16 forward
+  amplified by FP8 rounding flips (r05a: cosine 0.9979 for llama_fp8); this build's own amax may
+  cost at most twice that distance (a 1-ulp amax difference moves an FP8 scale).
 The launches per kernel family (``_ext.dispatch_counts``, the library's dispatch registry) are
 asserted, so the test fails if the production shapes stop reaching those kernels.
 """
@@ -102,7 +104,7 @@ def _run(name, gpu, monkeypatch):
     after = _ext.dispatch_counts()
     monkeypatch.setattr(MaxCalibrator, "collect", orig_collect)
     launched = {k: after[k] - before[k] for k in after if after[k] > before[k]}
-    return model, fp, logits, launched, seen
+    return model, fp, logits, launched, seen, test
 
 
 def _ulps(got: torch.Tensor, want: torch.Tensor) -> torch.Tensor:
@@ -119,7 +121,7 @@ def test_prod_e2e(gpu, golden, name, monkeypatch):
 
     t, meta = golden
     m = meta[name]
-    model, fp, logits, launched, seen = _run(name, gpu, monkeypatch)
+    model, fp, logits, launched, seen, test = _run(name, gpu, monkeypatch)
     assert fp == m["fingerprint"], "regenerated weights differ from the reference run's"
     print(f"{name}: library launches {launched}")
     missing = [k for k in EXPECTED_KERNELS[name] if not launched.get(k)]
@@ -170,7 +172,30 @@ def test_prod_e2e(gpu, golden, name, monkeypatch):
         assert same >= len(awq) - 2, f"best alpha differs on {len(awq) - same} of {len(awq)} linears"
 
     ref = t[f"{name}.logits"]
-    err = (logits - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
-    cos = torch.nn.functional.cosine_similarity(logits.flatten(), ref.flatten(), dim=0).item()
-    print(f"{name}: logits max rel err {err:.3e}, cosine {cos:.6f}")
-    assert err < 0.1 and cos > 0.999
+
+    def dist(lg):
+        err = (lg - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+        cos = torch.nn.functional.cosine_similarity(lg.flatten(), ref.flatten(), dim=0).item()
+        return err, cos
+
+    # noise floor: the same GPU forward with the reference run's own amax loaded into every
+    # quantizer it holds one for -- what remains is the GPU-vs-CPU bf16 forward (GEMM / SDPA /
+    # RMSNorm order), amplified by FP8 rounding flips, not this build's calibration
+    saved = {}
+    for n, q in quantizers.items():
+        key = f"{name}.amax.{n}"
+        if key in t:
+            saved[n] = q.amax.detach().clone()
+            q.amax = t[key].to(q.amax.device)
+    with torch.no_grad():
+        floor_logits = model(test.to(gpu)).logits.float().cpu()
+    for n, a in saved.items():
+        quantizers[n].amax = a
+    err, cos = dist(logits)
+    ferr, fcos = dist(floor_logits)
+    print(f"{name}: logits max rel err {err:.3e}, cosine {cos:.6f}; with the reference amax loaded "
+          f"({len(saved)} quantizers): {ferr:.3e}, {fcos:.6f}")
+    assert fcos > 0.99 and ferr < 0.2, "GPU forward with the reference's amax far from the reference logits"
+    # this build's amax cost at most twice the forward's own distance (plus a small absolute slack)
+    assert 1 - cos <= 2 * (1 - fcos) + 5e-4, (cos, fcos)
+    assert err <= 2 * ferr + 0.02, (err, ferr)
