@@ -342,6 +342,38 @@ template <> struct Fp4Native<_Float16> {
   }
 };
 
+// ---- native CDNA4 FP8 (E4M3) scaled converts on packed 16-bit pairs -------------------------------
+// v_cvt_scalef32_pk_fp8_{bf16,f16}: two 16-bit floats -> two E4M3 bytes of x / 2^e(s), written to
+// the low or high 16 bits of the destination (word_sel); v_cvt_scalef32_pk_{bf16,f16}_fp8: two E4M3
+// bytes (low / high half) -> code * 2^e(s).  Used only where the MX E4M3 block scale keeps
+// |x| / 2^e <= 448 (e8m0_scale) and the exponents in the range tests/test_gpu_mx_native.py checks
+// exhaustively against the emulated mx_vec_kernel path (every 16-bit pattern at every scale).
+typedef short i16x2_t __attribute__((ext_vector_type(2)));
+template <typename T> struct Fp8Native;
+template <> struct Fp8Native<__bf16> {
+  // w0, w1: two packed pairs -> four E4M3 bytes
+  static __device__ __forceinline__ uint32_t down(uint32_t w0, uint32_t w1, float s) {
+    i16x2_t p = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16((i16x2_t){0, 0}, __builtin_bit_cast(bf16x2_t, w0), s, false);
+    p = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(p, __builtin_bit_cast(bf16x2_t, w1), s, true);
+    return __builtin_bit_cast(uint32_t, p);
+  }
+  static __device__ __forceinline__ uint32_t up(uint32_t p, float s, bool hi) {
+    return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(p, s, true)
+                                           : __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(p, s, false));
+  }
+};
+template <> struct Fp8Native<_Float16> {
+  static __device__ __forceinline__ uint32_t down(uint32_t w0, uint32_t w1, float s) {
+    i16x2_t p = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16((i16x2_t){0, 0}, __builtin_bit_cast(f16x2_t, w0), s, false);
+    p = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(p, __builtin_bit_cast(f16x2_t, w1), s, true);
+    return __builtin_bit_cast(uint32_t, p);
+  }
+  static __device__ __forceinline__ uint32_t up(uint32_t p, float s, bool hi) {
+    return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(p, s, true)
+                                           : __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(p, s, false));
+  }
+};
+
 // Per-lane scan of 4 packed 16-bit pairs: the largest |x| pattern (NaN patterns sort above inf)
 // and whether any element is -0 (pattern 0x8000), two packed u16 ops per pair.
 struct PairScan {
@@ -418,7 +450,7 @@ enum DispatchId {
   kDispEwVec, kDispEwGroupSk, kDispEwGroup, kDispEwRowwave, kDispAmaxPersist, kDispAmaxRowsU,
   kDispAmaxRowsShort, kDispAmaxColsWide, kDispBlockQuantDyn, kDispHistValue, kDispHistValueChunked,
   kDispMxVec, kDispMxE2m1Native, kDispNvfp4NativeU, kDispAwqSearchPp, kDispAwqPrescale, kDispAwqMseMulti,
-  kDispHistNzBounds, kDispCount
+  kDispHistNzBounds, kDispMxE4m3Native, kDispCount
 };
 void count_dispatch(int id);
 

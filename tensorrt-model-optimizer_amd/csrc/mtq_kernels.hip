@@ -656,6 +656,71 @@ __global__ __launch_bounds__(kThreads) void mx_e2m1_native_kernel(const T *__res
   stg_vec_nt(y + i * N, v);
 }
 
+// MXFP8 (E4M3 elements, E8M0 scales, no global amax) on 16-bit inputs with the native CDNA4
+// scaled FP8 converts (Fp8Native): per two packed pairs one down-convert pair by the block's
+// unscale 2^e and one up-convert pair -- the emulated path's sign(x) * e4m3(|x| * scale) *
+// unscale (tensor_quant_mx.cu:36-55) in 4 instructions per 4 elements.  Block amax from packed
+// u16 max of the |x| patterns, as mx_e2m1_native_kernel; blocks with a NaN or an infinity, lanes
+// with a -0 and block exponents outside [kLo, kHi] take the emulated path, so every element is
+// bit-identical to mx_vec_kernel (checked exhaustively, tests/test_gpu_mx_native.py).  U = 2
+// vectors per lane, both loads issued first.
+template <typename T, int BS, int U>
+__global__ __launch_bounds__(kThreads) void mx_e4m3_native_kernel(const T *__restrict__ x,
+                                                                   T *__restrict__ y,
+                                                                   int64_t nvec) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  static_assert(N == 8 && BS % N == 0, "16-bit elements, block a multiple of the vector");
+  constexpr int LPB = BS / N;
+  constexpr int kLo = sizeof(T) == 2 && __is_same(T, _Float16) ? -30 : -125;
+  constexpr int kHi = sizeof(T) == 2 && __is_same(T, _Float16) ? 7 : 125;
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  const int lead = threadIdx.x % LPB;
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: see export_mxfp4_vec_kernel
+    const int64_t i = base + u * kThreads;
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * N);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kThreads;
+    if (i - lead >= nvec) continue;
+    uint32_t w[4] = {v[u].raw.x, v[u].raw.y, v[u].raw.z, v[u].raw.w};
+    const PairScan sc = scan_pairs(w);
+    const uint32_t mb = group_max_u32<LPB>(sc.max_abs);
+    const bool block_nan = mb > Fp4Native<T>::kInfBits;  // uniform over the block's lanes
+    float amax;
+    if (!block_nan) {
+      amax = mb == Fp4Native<T>::kInfBits ? 3.402823466e38f : half_bits_to_float<T>(mb);
+    } else {  // NaN is skipped by the reference's block max, as in mx_vec_kernel
+      float m = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) m = max_skip_nan(m, clamp_flt_max(fabsf(Elem<T>::ld(v[u].e[j]))));
+      amax = group_max_f<LPB>(m);
+    }
+    float scale, unscale;
+    e8m0_scale(amax, 448.0f, scale, unscale);
+    const int ue = (int)((__float_as_uint(unscale) >> 23) & 0xff) - 127;
+    // (a block holding +-inf: E4M3 has no infinity -- the convert gives NaN where the emulated
+    // path saturates to 448 -- so it is emulated too)
+    if (mb < Fp4Native<T>::kInfBits && !sc.neg_zero && ue >= kLo && ue <= kHi) {
+      const uint32_t p0 = Fp8Native<T>::down(w[0], w[1], unscale);
+      const uint32_t p1 = Fp8Native<T>::down(w[2], w[3], unscale);
+      w[0] = Fp8Native<T>::up(p0, unscale, false);
+      w[1] = Fp8Native<T>::up(p0, unscale, true);
+      w[2] = Fp8Native<T>::up(p1, unscale, false);
+      w[3] = Fp8Native<T>::up(p1, unscale, true);
+      v[u].raw = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        v[u].e[j] = Elem<T>::st(mx_qdq(Elem<T>::ld(v[u].e[j]), scale, unscale, MTQ_E4M3));
+    }
+    stg_vec_nt(y + i * N, v[u]);
+  }
+}
+
 template <typename T, int BS>
 void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t stream) {
   const unsigned g = (unsigned)((nvec + kThreads - 1) / kThreads);
@@ -663,6 +728,12 @@ void launch_mx_vec(const T *x, T *y, int64_t nvec, MxParams p, hipStream_t strea
     if (p.fmt == MTQ_E2M1 && p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
       count_dispatch(kDispMxE2m1Native);
       mx_e2m1_native_kernel<T, BS><<<g, kThreads, 0, stream>>>(x, y, nvec);
+      return;
+    }
+    if (p.fmt == MTQ_E4M3 && p.gamax == nullptr && p.sfmt == MTQ_E8M0) {
+      count_dispatch(kDispMxE4m3Native);
+      const unsigned g2 = (unsigned)((nvec + 2 * kThreads - 1) / (2 * kThreads));
+      mx_e4m3_native_kernel<T, BS, 2><<<g2, kThreads, 0, stream>>>(x, y, nvec);
       return;
     }
   }
@@ -868,17 +939,31 @@ __global__ __launch_bounds__(kThreads) void amax_fold_kernel(float *__restrict__
 
 // one workgroup: grid-stride flags, wave OR, LDS OR, thread 0 writes all three
 constexpr int kCheckThreads = 1024;
-template <typename T>
+__device__ __forceinline__ int check_bits(float v) {
+  return (v != v) | ((fabsf(v) == __builtin_inff()) << 1) | ((v < 0.f) << 2);
+}
+
+// bits of NaN / inf / negative over the block; MULTI: a grid-stride pass over 16-byte vectors
+// (x aligned, n % N elements past the last whole vector by block 0), OR-ed into flags zeroed by
+// amax_check_zero_kernel; else one block over scalars, writing flags
+template <typename T, bool MULTI>
 __global__ __launch_bounds__(kCheckThreads) void amax_check_kernel(const T *__restrict__ x, int64_t n,
                                                                   int32_t *__restrict__ flags) {
-  int nan = 0, inf = 0, neg = 0;
-  for (int64_t i = threadIdx.x; i < n; i += kCheckThreads) {
-    const float v = Elem<T>::ld(x[i]);
-    nan |= v != v;
-    inf |= fabsf(v) == __builtin_inff();
-    neg |= v < 0.f;
+  int bits = 0;
+  if constexpr (MULTI) {
+    using V = Vec<T>;
+    const int64_t nvec = n / V::N;
+    const int64_t stride = (int64_t)gridDim.x * kCheckThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kCheckThreads + threadIdx.x; i < nvec; i += stride) {
+      const V v = ldg_vec_nt(x + i * V::N);
+#pragma unroll
+      for (int j = 0; j < V::N; ++j) bits |= check_bits(Elem<T>::ld(v.e[j]));
+    }
+    if (blockIdx.x == 0)
+      for (int64_t i = nvec * V::N + threadIdx.x; i < n; i += kCheckThreads) bits |= check_bits(Elem<T>::ld(x[i]));
+  } else {
+    for (int64_t i = threadIdx.x; i < n; i += kCheckThreads) bits |= check_bits(Elem<T>::ld(x[i]));
   }
-  int bits = nan | (inf << 1) | (neg << 2);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) bits |= __shfl_xor(bits, o);
   __shared__ int red[kCheckThreads / 64];
@@ -886,10 +971,19 @@ __global__ __launch_bounds__(kCheckThreads) void amax_check_kernel(const T *__re
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < kCheckThreads / 64; ++w) bits |= red[w];
-    flags[0] = bits & 1;
-    flags[1] = (bits >> 1) & 1;
-    flags[2] = (bits >> 2) & 1;
+    if constexpr (MULTI) {
+      for (int k = 0; k < 3; ++k)
+        if ((bits >> k) & 1) atomicOr(flags + k, 1);
+    } else {
+      flags[0] = bits & 1;
+      flags[1] = (bits >> 1) & 1;
+      flags[2] = (bits >> 2) & 1;
+    }
   }
+}
+
+__global__ void amax_check_zero_kernel(int32_t *flags) {
+  if (threadIdx.x < 3) flags[threadIdx.x] = 0;
 }
 
 // y[r, :] = x[r, :] if any of row r's k expert indices lies in [0, E), else +0 (the MoE shared
@@ -2523,10 +2617,11 @@ __device__ __forceinline__ void export_mxfp4_vec_one(int64_t i, const Vec<T> &v,
 // and all U vectors of a lane loaded before the first is converted.  Same arithmetic as
 // export_fp8_vec_one: div_rn on packed pairs, optional re-rounding, the native RNE convert for
 // |q| <= 448, the exact per-element form for a lane with an overflowing or NaN quotient.
+// the E4M3 bytes of one 16-bit vector (8 elements), packed in two dwords
 template <typename T, bool ROUND>
-__device__ __forceinline__ void export_fp8_pt_one(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y,
-                                                  float s, float r) {
-  constexpr int N = Vec<T>::N;
+__device__ __forceinline__ u32x2_t export_fp8_pt_pack(const Vec<T> &v, float s, float r) {
+  static_assert(Vec<T>::N == 8, "16-bit vectors");
+  constexpr int N = 8;
   float q[N];
   bool inrange = true;
 #pragma unroll
@@ -2538,17 +2633,13 @@ __device__ __forceinline__ void export_fp8_pt_one(int64_t i, const Vec<T> &v, ui
     inrange &= (fabsf(d.x) <= kE4M3Max) & (fabsf(d.y) <= kE4M3Max);
   }
   if (__builtin_expect(inrange, 1)) {
-    uint32_t w[N / 4];
+    uint32_t w[2];
 #pragma unroll
-    for (int k = 0; k < N / 4; ++k) {
+    for (int k = 0; k < 2; ++k) {
       int p = __builtin_amdgcn_cvt_pk_fp8_f32(q[4 * k], q[4 * k + 1], 0, false);
       w[k] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(q[4 * k + 2], q[4 * k + 3], p, true);
     }
-    if constexpr (N == 8)
-      st_packed_nt(y + i * N, w[0], w[1]);
-    else
-      st_packed_nt(y + i * N, w[0]);
-    return;
+    return (u32x2_t){w[0], w[1]};
   }
   uint32_t b[N];
 #pragma unroll
@@ -2557,12 +2648,44 @@ __device__ __forceinline__ void export_fp8_pt_one(int64_t i, const Vec<T> &v, ui
     if constexpr (ROUND) qq = Elem<T>::ld(Elem<T>::st(qq));
     b[j] = e4m3_byte(qq) | nan_sign_byte(v.e[j]);
   }
-  if constexpr (N == 8)
-    st_packed_nt(y + i * N, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
-                 b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
-  else
-    st_packed_nt(y + i * N, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
+  return (u32x2_t){b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24), b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24)};
 }
+
+template <typename T, bool ROUND>
+__device__ __forceinline__ void export_fp8_pt_one(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y,
+                                                  float s, float r) {
+  constexpr int N = Vec<T>::N;
+  if constexpr (N == 8) {
+    const u32x2_t w = export_fp8_pt_pack<T, ROUND>(v, s, r);
+    st_packed_nt(y + i * N, w.x, w.y);
+    return;
+  } else {
+    float q[N];
+    bool inrange = true;
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      f32x2_t d = div_rn2((f32x2_t){Elem<T>::ld(v.e[j]), Elem<T>::ld(v.e[j + 1])}, s, r);
+      if constexpr (ROUND) d = round_pair<T>(d);
+      q[j] = d.x;
+      q[j + 1] = d.y;
+      inrange &= (fabsf(d.x) <= kE4M3Max) & (fabsf(d.y) <= kE4M3Max);
+    }
+    if (__builtin_expect(inrange, 1)) {
+      int p = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+      st_packed_nt(y + i * N, (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], p, true));
+      return;
+    }
+    uint32_t b[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      float qq = div_rn(Elem<T>::ld(v.e[j]), s, r);
+      if constexpr (ROUND) qq = Elem<T>::ld(Elem<T>::st(qq));
+      b[j] = e4m3_byte(qq) | nan_sign_byte(v.e[j]);
+    }
+    st_packed_nt(y + i * N, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
+  }
+}
+
 template <int U, typename T, bool ROUND>
 __global__ __launch_bounds__(kThreads) void export_fp8_pt_kernel(const T *__restrict__ x,
                                                                   uint8_t *__restrict__ y,
@@ -2742,7 +2865,7 @@ void count_dispatch(int id) { g_dispatch[id].fetch_add(1, std::memory_order_rela
 static const char *const kDispatchNames[kDispCount] = {
     "ew_vec", "ew_group_sk", "ew_group", "ew_rowwave", "amax_persist", "amax_rows_u", "amax_rows_short",
     "amax_cols_wide", "block_quant_dyn", "hist_value", "hist_value_chunked", "mx_vec", "mx_e2m1_native",
-    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_nz_bounds"};
+    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_nz_bounds", "mx_e4m3_native"};
 }  // namespace mtq
 
 // ============================================================================================
@@ -2885,7 +3008,18 @@ int mtq_amax_check(const void *x, int64_t n, int dtype, int32_t *flags, hipStrea
   if (n < 0 || !flags || (n > 0 && !x)) return MTQ_ERR_INVALID_ARG;
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
-    amax_check_kernel<T><<<1, kCheckThreads, 0, stream>>>(reinterpret_cast<const T *>(x), n, flags);
+    // one workgroup up to 1 M elements (one launch, no zeroing); above, the whole GPU (static
+    // block scales concatenated over many quantizers reach 10^8 elements: ADVICE r04)
+    if (n <= (1 << 20) || !aligned16(x)) {
+      amax_check_kernel<T, false><<<1, kCheckThreads, 0, stream>>>(reinterpret_cast<const T *>(x), n, flags);
+    } else {
+      const int64_t nvec = n / Vec<T>::N;
+      int64_t g = (nvec + (int64_t)kCheckThreads * 4 - 1) / ((int64_t)kCheckThreads * 4);
+      const int64_t cap = (int64_t)num_cus() * 2;
+      g = g < cap ? g : cap;
+      amax_check_zero_kernel<<<1, 64, 0, stream>>>(flags);
+      amax_check_kernel<T, true><<<(unsigned)g, kCheckThreads, 0, stream>>>(reinterpret_cast<const T *>(x), n, flags);
+    }
     return check_launch();
   });
 }

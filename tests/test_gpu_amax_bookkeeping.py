@@ -32,8 +32,12 @@ def test_fill_fold_match_torch(gpu):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_check_flags(gpu, dtype):
     ops = _ext.ops()
-    for n in (1, 1000, 70001):
-        x = (torch.rand(n, device=gpu) + 0.5).to(dtype)
+    # above 2^20 elements the grid-stride form (zeroed flags, 16-byte vectors, a ragged tail);
+    # the [1:] view is not 16-byte aligned: the one-workgroup form
+    for n in (1, 1000, 70001, (1 << 20) + 1, 3_000_007, -3_000_001):
+        x = (torch.rand(abs(n) + (n < 0), device=gpu) + 0.5).to(dtype)
+        if n < 0:
+            x, n = x[1:], -n
         assert ops.amax_check(x).tolist() == [0, 0, 0]
         for pos, val, flag in ((n - 1, math.nan, 0), (n // 2, -math.inf, 1), (0, -0.25, 2)):
             y = x.clone()
