@@ -188,9 +188,12 @@ def kernel_suite(ops, xs, steps, warmup):
         "nvfp4_block16_dynamic": (lambda x: ops.nvfp4_fake_quant_block(x, amax_t, 16), 4),
         # checkpoint export packing: bf16 read + packed bytes written
         "export_fp8_per_tensor": (lambda x: ops.export_fp8(x, fp8_s, False, True), 3),
-        "export_nvfp4_pack": (lambda x: ops.export_nvfp4(x, nv_bs, nv_s2), 2.5),
-        "export_int4_pack": (lambda x: ops.export_int4(x, i4_s), 2.5),
-        "export_mxfp4_pack": (lambda x: ops.export_mxfp4(x, 32)[0], 2.5),
+        # (bytes per element: bf16 in + packed codes out + the block scales read / written --
+        # NVFP4 fp32 per 16, INT4 fp32 per 128, MXFP4 E8M0 bytes per 32 -- each input with its own
+        # scale tensor, as every weight of a real export has)
+        "export_nvfp4_pack": (lambda x: ops.export_nvfp4(x, nv_bs[ix(x)], nv_s2), 2.5 + 4 / 16),
+        "export_int4_pack": (lambda x: ops.export_int4(x, i4_s[ix(x)]), 2.5 + 4 / 128),
+        "export_mxfp4_pack": (lambda x: ops.export_mxfp4(x, 32)[0], 2.5 + 1 / 32),
         "amax_per_tensor": (None, 2),
         # K6 per-row (axis 0 kept) and per-column (axis -1 kept) running amax, K7 histogram
         "amax_per_row": (lambda x: ops.amax_accumulate(x, acc_r, 1, x.shape[0], x.shape[1]) or acc_r, 2),
@@ -201,7 +204,12 @@ def kernel_suite(ops, xs, steps, warmup):
     acc_c = torch.zeros(xs[0].shape[1], device="cuda")
     hmax = torch.tensor([16.0 * 6], device="cuda")
     counts = torch.zeros(2048, dtype=torch.int32, device="cuda")
-    nv_bs = torch.ones(xs[0].numel() // 16, device="cuda")
+    ids = [id(t) for t in xs]
+
+    def ix(x):
+        return ids.index(id(x))
+
+    nv_bs = [torch.ones(x.numel() // 16, device="cuda") for x in xs]
     # the packers' scale inputs, computed once (a per-call division would time a second launch).
     # FP8 export: the scale an export derives from the tensor itself, amax / 448 (quant_utils.py
     # per-tensor weight scale; one scale over the 4 rotating inputs), so no quotient passes 448 --
@@ -209,7 +217,7 @@ def kernel_suite(ops, xs, steps, warmup):
     # and a quarter of the waves ran the exact out-of-range path (0.72 vs 0.78-0.79, r05k)
     fp8_s = torch.stack([x.abs().amax().float() for x in xs]).amax() / 448
     nv_s2 = amax_t / 2688
-    i4_s = torch.full((xs[0].shape[0], xs[0].shape[1] // 128), 0.01, device="cuda")
+    i4_s = [torch.full((x.shape[0], x.shape[1] // 128), 0.01, device="cuda") for x in xs]
     acc = torch.zeros(1, device="cuda")
     for name, (fn, bpe) in cases.items():
         if fn is None:

@@ -413,7 +413,20 @@ __global__ __launch_bounds__(kThreads) void ew_rowwave_kernel(const T *__restric
   }
   if (wb >= nvec) return;
   const int64_t c = wb / vb;  // wave-uniform (scalar)
-  const auto q = op.qparam_from((float)amax[c]);
+  float am;
+  if constexpr (sizeof(A) == 2) {
+    // a 16-bit amax through the scalar cache: the dword holding it (s_load_dword; gfx950 has no
+    // 16-bit scalar load, and the vector load the compiler emits otherwise put a VMEM round trip
+    // in front of every wave's first store: 0.746 vs 0.777 with an fp32 amax, r05n).  amax is
+    // 4-byte aligned (the launcher checks), so the dword of an even-count tensor's last element
+    // is inside it and an odd count's last dword ends 2 bytes past it, inside the allocation.
+    const uint32_t wv = reinterpret_cast<const uint32_t *>(amax)[c >> 1];
+    const uint16_t h = (uint16_t)((c & 1) ? (wv >> 16) : (wv & 0xFFFFu));
+    am = Elem<A>::ld(__builtin_bit_cast(A, h));
+  } else {
+    am = (float)amax[c];
+  }
+  const auto q = op.qparam_from(am);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = wb + u * 64 + lane;
@@ -482,8 +495,9 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
     }
     // long channels (per-row weights): channel length a multiple of 128 vectors, fp32 amax,
     // 16-byte aligned, no outer wrap -> wave-uniform channel
-    const bool amax_own = (op.amax_dtype == MTQ_BF16 && __is_same(T, __bf16)) ||
-                          (op.amax_dtype == MTQ_F16 && __is_same(T, _Float16));
+    const bool amax_own = ((op.amax_dtype == MTQ_BF16 && __is_same(T, __bf16)) ||
+                           (op.amax_dtype == MTQ_F16 && __is_same(T, _Float16))) &&
+                          reinterpret_cast<uintptr_t>(op.amax) % 4 == 0;
     if (vb >= 128 && vb % 128 == 0 && aligned16(x) && aligned16(y) &&
         (op.amax_dtype == MTQ_F32 || amax_own) && axis_size * vb == n / N && n % N == 0) {
       constexpr int U = 2;
@@ -3098,7 +3112,9 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
     const size_t shm = lds ? (size_t)bins * 4 : 0;
     // 16-bit dtypes: pattern histogram + per-block fold, U = 2 vectors per lane with a register
     // prefetch (bf16 [32768, 4096], 2048 bins: 46.9 us = 71.6 %; U 1 / 4 / 8 and no prefetch
-    // measured no faster, profiles/r02/histogram/).
+    // measured no faster, profiles/r02/histogram/; r05: U 4 / 2 / 3 = 40.0 / 41.3 / 46.0 us on
+    // bf16 [8192, 14336] (profiles/r05/hist/hist_u_ab_r05m.log) but 0.691 vs 0.73-0.74 on the
+    // bench input and slower for the chunked form (r05n), so U stays 2).
     if constexpr (sizeof(T) == 2) {
       if (aligned16(x) && n % N == 0 && bins <= 8192) {
         const int64_t nvec = n / N;
