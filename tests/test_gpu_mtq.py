@@ -47,8 +47,12 @@ def _tiny_llama():
     return LlamaForCausalLM(cfg).eval()
 
 
-def test_c2_tiny_llama_fp8(gpu):
+def test_c2_tiny_llama_fp8(gpu, monkeypatch):
+    """Weight amax bit-exact vs the reference run; activation amax bit-exact vs torch's max|x| over
+    the very tensors each quantizer collected on the GPU, and within rtol 1e-5 of the reference's
+    (its CPU fp32 forward vs the GPU's GEMM / SDPA summation order)."""
     import modelopt_amd.torch.quantization as mtq
+    from modelopt_amd.torch.quantization.calib.max import MaxCalibrator
 
     t = load_file(str(G / "llama_fp8.safetensors"))
     model = _tiny_llama()
@@ -60,15 +64,32 @@ def test_c2_tiny_llama_fp8(gpu):
         for b in ids:
             mm(b)
 
+    seen = {}
+    orig = MaxCalibrator.collect
+
+    def spy(self, x):
+        if self._axis is None and x.numel():
+            a = x.detach().abs().amax().float()
+            seen[id(self)] = torch.maximum(seen[id(self)], a) if id(self) in seen else a
+        return orig(self, x)
+
+    monkeypatch.setattr(MaxCalibrator, "collect", spy)
     mtq.quantize(model, mtq.FP8_DEFAULT_CFG, loop)
-    got = {n: q.amax for n, q in model.named_modules() if isinstance(q, mtq.TensorQuantizer) and q.amax is not None}
+    monkeypatch.setattr(MaxCalibrator, "collect", orig)
+    qs = {n: q for n, q in model.named_modules() if isinstance(q, mtq.TensorQuantizer) and q.amax is not None}
+    got = {n: q.amax for n, q in qs.items()}
     want = {k[5:]: v for k, v in t.items() if k.startswith("amax.")}
     assert set(got) == set(want)
+    self_checked = 0
     for n, v in want.items():
+        if id(qs[n]._calibrator) in seen:
+            assert torch.equal(got[n].float().reshape(()), seen[id(qs[n]._calibrator)].to(got[n].dtype).float()), n
+            self_checked += 1
         if "weight_quantizer" in n:
             assert torch.equal(got[n].cpu(), v), n
         else:
             torch.testing.assert_close(got[n].cpu(), v, rtol=1e-5, atol=1e-6)
+    assert self_checked >= len([n for n in want if "input_quantizer" in n])
     logits = model(t["test_ids"].to(gpu)).logits.detach().cpu()
     torch.testing.assert_close(logits, t["logits"], rtol=2e-3, atol=2e-3)
 
