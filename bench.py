@@ -194,6 +194,7 @@ def kernel_suite(ops, xs, steps, warmup):
         "export_nvfp4_pack": (lambda x: ops.export_nvfp4(x, nv_bs[ix(x)], nv_s2), 2.5 + 4 / 16),
         "export_int4_pack": (lambda x: ops.export_int4(x, i4_s[ix(x)]), 2.5 + 4 / 128),
         "export_mxfp4_pack": (lambda x: ops.export_mxfp4(x, 32)[0], 2.5 + 1 / 32),
+        "export_fp8_block2d_128": (lambda x: ops.export_fp8_block2d(x, b2d_s[ix(x)], 128, 128), 3 + 4 / 16384),
         "amax_per_tensor": (None, 2),
         # K6 per-row (axis 0 kept) and per-column (axis -1 kept) running amax, K7 histogram
         "amax_per_row": (lambda x: ops.amax_accumulate(x, acc_r, 1, x.shape[0], x.shape[1]) or acc_r, 2),
@@ -218,6 +219,8 @@ def kernel_suite(ops, xs, steps, warmup):
     fp8_s = torch.stack([x.abs().amax().float() for x in xs]).amax() / 448
     nv_s2 = amax_t / 2688
     i4_s = [torch.full((x.shape[0], x.shape[1] // 128), 0.01, device="cuda") for x in xs]
+    # FP8_PB_WO export: each input's own 128 x 128 block amax / 448 (fp32), as the export derives it
+    b2d_s = [x.view(x.shape[0] // 128, 128, x.shape[1] // 128, 128).abs().amax(dim=(1, 3)).float() / 448 for x in xs]
     acc = torch.zeros(1, device="cuda")
     for name, (fn, bpe) in cases.items():
         if fn is None:

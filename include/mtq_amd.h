@@ -271,6 +271,16 @@ size_t mtq_qlinear_small_m_group_workspace_bytes(int64_t M, const int64_t *N, in
 int mtq_qlinear_small_m_group(const mtq_qlinear_problem *problems, int n, int64_t M, int64_t K,
                               int dtype, void *ws, size_t ws_bytes, hipStream_t stream);
 
+/* FP8 (E4M3) bytes of a [rows, cols] weight with 2D block scales: y = e4m3(x / scale[r / block_rows,
+ * c / block_cols]) (FP8QTensor.quantize(w, s, block_sizes={-1: bc, -2: br}),
+ * qtensor/fp8_tensor.py:40-117; the FP8_PB_WO export, export/quant_utils.py:874-877): the fp32
+ * quotient, or with round_to_dtype the quotient rounded to the weight's 16-bit dtype first (a
+ * scale tensor in the weight's own dtype: torch divides in that dtype).  scale: fp32 values
+ * [ceil(rows / block_rows), ceil(cols / block_cols)] contiguous; cols and block_cols multiples of
+ * the 16-byte vector (8 bf16 / f16, 4 fp32), x 16-byte aligned (MTQ_ERR_INVALID_ARG otherwise). */
+int mtq_export_fp8_block2d(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype, const float *scale,
+                           int64_t block_rows, int64_t block_cols, int round_to_dtype, hipStream_t stream);
+
 /* ---- checkpoint export (real-quant packing) ----------------------------------------------
  * export/quant_utils.py:836-938 to_quantized_weight and the qtensor quantize() routines; weights
  * [rows, cols] row-major of dtype, outputs raw bytes.

@@ -2308,6 +2308,9 @@ template <typename T> __device__ __forceinline__ f32x2_t round_pair(f32x2_t d) {
   }
 }
 
+template <typename T>
+__device__ __forceinline__ void export_fp8_pack_store(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y, float s,
+                                                      int round_dtype, int native);
 template <typename T, bool IDX32>
 __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restrict__ x,
                                                                    uint8_t *__restrict__ y,
@@ -2322,6 +2325,16 @@ __device__ __forceinline__ void export_fp8_vec_one(int64_t i, const T *__restric
   V v = ldg_vec_nt(x + i * N);
   // per-tensor: the scalar-loaded s_t (no per-lane load and its latency before the division)
   const float s = per_row ? scale[idx_div<IDX32>(i, cv, fcv)] : s_t;
+  export_fp8_pack_store<T>(i, v, y, s, round_dtype, native);
+}
+
+// the E4M3 bytes of vector i of x (loaded in v) divided by s, stored at y + i * N: the packed RNE
+// convert where every quotient of the vector is within +-448, the exact per-element path otherwise
+template <typename T>
+__device__ __forceinline__ void export_fp8_pack_store(int64_t i, const Vec<T> &v, uint8_t *__restrict__ y, float s,
+                                                      int round_dtype, int native) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
   const float r = 1.0f / s;
   uint32_t b[N];
   if (native) {
@@ -2744,6 +2757,24 @@ __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__res
     export_fp8_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cv, fcv, scale, per_row, round_dtype,
                                  native, s_t);
 }
+// FP8 with 2D block scales (FP8QTensor.quantize with {-1: bc, -2: br}, qtensor/fp8_tensor.py:40-117,
+// the FP8_PB_WO export, export/quant_utils.py:874-877): vector i (N elements along a row, never
+// across a column block: bc % N == 0) uses scale[(row / br) * ncb + col / bc] of the fp32 block
+// grid; the fp32 quotient (input / expanded_scales promotes to fp32) converted as the per-row path.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void export_fp8_blk2d_kernel(const T *__restrict__ x, uint8_t *__restrict__ y,
+                                                                    int64_t nvec, int64_t cv, int64_t br, int64_t bcv,
+                                                                    int64_t ncb, const float *__restrict__ scale,
+                                                                    int round_dtype, int native) {
+  constexpr int N = Vec<T>::N;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= nvec) return;
+  const Vec<T> v = ldg_vec_nt(x + i * N);
+  const int64_t row = i / cv, cvec = i - row * cv;
+  const float s = scale[(row / br) * ncb + cvec / bcv];
+  export_fp8_pack_store<T>(i, v, y, s, round_dtype, native);
+}
+
 template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__restrict__ x,
                                                                     uint8_t *__restrict__ y,
@@ -3353,6 +3384,24 @@ int mtq_export_fp8(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dt
       export_fp8_kernel<T><<<grid_for(n, kThreads), kThreads, 0, stream>>>(
           reinterpret_cast<const T *>(x), y, n, cols, scale, per_row, round_to_dtype);
     }
+    return check_launch();
+  });
+}
+
+int mtq_export_fp8_block2d(const void *x, uint8_t *y, int64_t rows, int64_t cols, int dtype, const float *scale,
+                           int64_t block_rows, int64_t block_cols, int round_to_dtype, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || block_rows < 1 || block_cols < 1) return MTQ_ERR_INVALID_ARG;
+  if (rows * cols == 0) return MTQ_OK;
+  if (!x || !y || !scale) return MTQ_ERR_INVALID_ARG;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    constexpr int N = Vec<T>::N;
+    if (cols % N != 0 || block_cols % N != 0 || !aligned16(x) || ((uintptr_t)y % N) != 0)
+      return MTQ_ERR_INVALID_ARG;
+    const int64_t nvec = rows * cols / N, cv = cols / N;
+    const int64_t ncb = (cols + block_cols - 1) / block_cols;
+    export_fp8_blk2d_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
+        reinterpret_cast<const T *>(x), y, nvec, cv, block_rows, block_cols / N, ncb, scale, round_to_dtype, 1);
     return check_launch();
   });
 }

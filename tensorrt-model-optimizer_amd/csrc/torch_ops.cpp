@@ -609,6 +609,29 @@ at::Tensor export_fp8(const at::Tensor &weight, const at::Tensor &scale, bool pe
   return y.view(at::kFloat8_e4m3fn);
 }
 
+// FP8 with 2D block scales (FP8QTensor.quantize with {-1: bc, -2: br}): scale [R, C] block grid of
+// a 2-D weight (any shape with that many elements); the quotient in the scale's dtype when it is
+// the weight's 16-bit dtype (torch's bf16 / bf16 division), fp32 otherwise
+at::Tensor export_fp8_block2d(const at::Tensor &weight, const at::Tensor &scale, int64_t block_rows,
+                              int64_t block_cols) {
+  check_device(weight, "weight");
+  const int dt = checked_dtype(weight, "weight");
+  TORCH_CHECK(dt != MTQ_F64 && weight.dim() == 2, "export_fp8_block2d: 2-D f32/f16/bf16 weight expected");
+  at::Tensor x = weight.contiguous();
+  const int64_t rows = x.size(0), cols = x.size(1);
+  TORCH_CHECK(block_rows >= 1 && block_cols >= 1, "export_fp8_block2d: block sizes");
+  const int64_t nrb = (rows + block_rows - 1) / block_rows, ncb = (cols + block_cols - 1) / block_cols;
+  TORCH_CHECK(scale.numel() == nrb * ncb, "export_fp8_block2d: scale must hold one value per block");
+  const bool round = scale.scalar_type() == weight.scalar_type() && dt != MTQ_F32;
+  at::Tensor s = scale.to(x.device(), at::kFloat).contiguous();
+  at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_status(mtq_export_fp8_block2d(x.data_ptr(), y.data_ptr<uint8_t>(), rows, cols, dt, s.data_ptr<float>(),
+                                      block_rows, block_cols, round ? 1 : 0, cur_stream(x)),
+               "export_fp8_block2d");
+  return y.view(at::kFloat8_e4m3fn);
+}
+
 at::Tensor export_int4(const at::Tensor &weight, const at::Tensor &scale) {
   check_device(weight, "weight");
   const int dt = checked_dtype(weight, "weight");
@@ -1142,6 +1165,7 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
   m.def("fp4_block_scale_quant(Tensor inputs, Tensor scales) -> Tensor");
   m.def("export_fp8(Tensor weight, Tensor scale, bool per_row, bool round_to_dtype) -> Tensor");
+  m.def("export_fp8_block2d(Tensor weight, Tensor scale, int block_rows, int block_cols) -> Tensor");
   m.def("export_int4(Tensor weight, Tensor scale) -> Tensor");
   m.def("export_nvfp4(Tensor weight, Tensor block_scale, Tensor scale_2) -> Tensor");
   m.def("export_mxfp4(Tensor weight, int block) -> (Tensor, Tensor)");
@@ -1186,6 +1210,7 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);
   m.impl("fp4_block_scale_quant", &fp4_block_scale_quant);
   m.impl("export_fp8", &export_fp8);
+  m.impl("export_fp8_block2d", &export_fp8_block2d);
   m.impl("export_int4", &export_int4);
   m.impl("export_nvfp4", &export_nvfp4);
   m.impl("export_mxfp4", &export_mxfp4);

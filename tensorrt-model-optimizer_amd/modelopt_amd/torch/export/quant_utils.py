@@ -310,9 +310,38 @@ def to_quantized_weight(weight, weights_scaling_factor, quantization, weights_sc
         return ops.export_fp8(weight, weights_scaling_factor, False, weights_scaling_factor.dim() == 0)
     if quantization in (QUANTIZATION_INT8_SQ, QUANTIZATION_INT8_WO):
         return (weight / weights_scaling_factor[:, None]).round().clamp(-128, 127).to(torch.int8)
+    if quantization == QUANTIZATION_FP8_PB_WO:
+        # FP8QTensor.quantize with {-1: bs, -2: bs} blocks (reference :874-877): the 2D-block
+        # packer divides by the scale of the weight's (row block, column block)
+        from ..quantization.qtensor import FP8QTensor
+
+        return FP8QTensor.quantize(
+            weight, weights_scaling_factor.squeeze(), block_sizes={-1: block_size, -2: block_size}
+        )[0]._quantized_data
     if quantization == QUANTIZATION_FP8_PC_PT:
         if weight.dim() == 3:
-            return (weight / weights_scaling_factor.unsqueeze(-1)).to(torch.float8_e4m3fn)
+            # per-expert scales (reference :880-906): [E] -> [E, 1, 1]; [E, C] matched against the
+            # input (BMM-style, [E, 1, K]) or the output dimension ([E, N, 1])
+            if weights_scaling_factor.dim() == 1:
+                return (weight / weights_scaling_factor[:, None, None]).to(torch.float8_e4m3fn)
+            if weights_scaling_factor.dim() == 2:
+                if weights_scaling_factor.shape[0] != weight.shape[0]:
+                    raise ValueError(
+                        "First dimension (num_experts) mismatch for FP8_PC_PT quantization. "
+                        f"weight shape: {weight.shape}, scale shape: {weights_scaling_factor.shape}")
+                if weight.shape[-1] == weight.shape[-2]:
+                    raise ValueError(
+                        "Ambiguous scaling dimension for FP8_PC_PT quantization with square weight matrix. "
+                        f"weight shape: {weight.shape}, scale shape: {weights_scaling_factor.shape}. "
+                        "Cannot determine if scaling should be applied to input_dim or output_dim.")
+                if weights_scaling_factor.shape[-1] == weight.shape[-1]:
+                    return (weight / weights_scaling_factor.unsqueeze(-2)).to(torch.float8_e4m3fn)
+                if weights_scaling_factor.shape[-1] == weight.shape[-2]:
+                    return (weight / weights_scaling_factor.unsqueeze(-1)).to(torch.float8_e4m3fn)
+                raise ValueError(
+                    "Cannot determine correct unsqueeze dimension for FP8_PC_PT quantization. "
+                    f"weight shape: {weight.shape}, scale shape: {weights_scaling_factor.shape}")
+            return (weight / weights_scaling_factor[:, None]).to(torch.float8_e4m3fn)  # reference :907
         return ops.export_fp8(weight, weights_scaling_factor, True, False)
     if quantization in (QUANTIZATION_INT4_AWQ, QUANTIZATION_W4A8_AWQ):
         return pack_int4_in_uint8(weight, weights_scaling_factor)
@@ -332,6 +361,8 @@ def to_quantized_weight(weight, weights_scaling_factor, quantization, weights_sc
         # same E8M0 scale from the weight; a scale from elsewhere takes the tensor expression
         from ..quantization.qtensor import MXFP8QTensor
 
+        if weight.dtype not in (torch.bfloat16, torch.float16):  # the packer takes 16-bit weights
+            return MXFP8QTensor.quantize_with_scale(weight, weights_scaling_factor)
         q, s = ops.export_mxfp8(weight)
         if weights_scaling_factor is not None and not torch.equal(s, weights_scaling_factor.reshape(s.shape)):
             q = MXFP8QTensor.quantize_with_scale(weight, weights_scaling_factor)

@@ -69,6 +69,19 @@ class FP8QTensor(BaseQuantizedTensor):
             if scales.shape != tuple(expected) and scales.numel() == math.prod(expected):
                 scales = scales.reshape(expected)
                 expanded = expanded.reshape(expected)
+            assert scales.shape == tuple(expected), (
+                f"Mismatch in expected scale shape: {scales.shape} vs {tuple(expected)}")
+            bs2 = {(d if d >= 0 else input.dim() + d): b for d, b in block_sizes.items()}
+            vec = 16 // original.element_size()
+            if (original.dim() == 2 and set(bs2) == {0, 1} and original.is_cuda
+                    and original.dtype in (torch.bfloat16, torch.float16, torch.float32)
+                    and scales.dtype in (torch.float32, original.dtype)
+                    and original.shape[1] % vec == 0 and bs2[1] % vec == 0
+                    and original.data_ptr() % 16 == 0):
+                # the 2D-block packer (one pass; the expression below materialises the expanded
+                # scales and the fp32 quotient): same quotient dtype and RNE convert
+                q = _ops().export_fp8_block2d(original, scales, bs2[0], bs2[1])
+                return cls(original.shape, original.dtype, q), scales
             for dim, bs in block_sizes.items():
                 expanded = expanded.repeat_interleave(bs, dim=dim)
         q = (input / expanded).to(torch.float8_e4m3fn)

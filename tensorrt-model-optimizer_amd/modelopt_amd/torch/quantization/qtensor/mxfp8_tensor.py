@@ -18,9 +18,24 @@ class MXFP8QTensor(BaseQuantizedTensor):
     SCALE_DTYPE = torch.uint8
 
     @classmethod
+    def _e8m0_from_weight(cls, weight: torch.Tensor) -> torch.Tensor:
+        """The reference's expression (reduce_block_amax, _compute_e8m0_exponent, :38-92) on the
+        device, for the weight dtypes the HIP packer does not take (fp32): ceil(log2(amax / 448))
+        clamped to [-127, 127], -127 where amax / 448 is not > 0, biased by 127."""
+        nb = weight.shape[-1] // cls.BLOCK_SIZE
+        amax = weight.reshape(*weight.shape[:-1], nb, cls.BLOCK_SIZE).abs().amax(dim=-1)
+        descale = amax.float() / cls.E4M3_MAX
+        lg = torch.where(descale > 0, torch.log2(descale), torch.tensor(-127.0, device=descale.device))
+        return (torch.clamp(torch.ceil(lg), min=-127, max=127) + 127).to(cls.SCALE_DTYPE)
+
+    @classmethod
     def get_weights_scaling_factor(cls, weight: torch.Tensor) -> torch.Tensor:
         assert weight.dim() >= 2, f"Weight must be at least 2D, got {weight.dim()}D"
-        return _ops().export_mxfp8(weight)[1]
+        assert weight.shape[-1] % cls.BLOCK_SIZE == 0, (
+            f"Weight inner dimension ({weight.shape[-1]}) must be divisible by MXFP8 block size ({cls.BLOCK_SIZE})")
+        if weight.dtype in (torch.bfloat16, torch.float16):
+            return _ops().export_mxfp8(weight)[1]
+        return cls._e8m0_from_weight(weight)
 
     @classmethod
     def get_weights_scaling_factor_from_quantizer(cls, weight: torch.Tensor, weight_quantizer) -> torch.Tensor:
@@ -47,8 +62,10 @@ class MXFP8QTensor(BaseQuantizedTensor):
     @classmethod
     def quantize(cls, input: torch.Tensor, weights_scaling_factor: torch.Tensor | None = None):
         if weights_scaling_factor is None and input.shape[-1] % cls.BLOCK_SIZE == 0:
-            q, s = _ops().export_mxfp8(input)
-            return cls(input.shape, input.dtype, q), s
+            if input.dtype in (torch.bfloat16, torch.float16):
+                q, s = _ops().export_mxfp8(input)
+                return cls(input.shape, input.dtype, q), s
+            weights_scaling_factor = cls._e8m0_from_weight(input)
         assert weights_scaling_factor is not None, "MXFP8: last dim must be a multiple of 32"
         return cls(input.shape, input.dtype, cls.quantize_with_scale(input, weights_scaling_factor)), weights_scaling_factor
 

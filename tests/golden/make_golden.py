@@ -632,11 +632,14 @@ EXPORT_CASES = {
     "w4a8_awq": "W4A8_AWQ_BETA_CFG",
     "nvfp4": "NVFP4_DEFAULT_CFG",
     "mxfp4": "MXFP4_DEFAULT_CFG",
+    "mxfp8": "MXFP8_DEFAULT_CFG",
+    "fp8_pb_wo": "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG",
 }
 
 
 def export_cfg(name):
-    """The preset, with INT4 groups of 32 so the tiny model (hidden 64) has two per row."""
+    """The preset, with INT4 groups of 32 so the tiny model (hidden 64) has two per row, and FP8 2D
+    blocks of 32 x 32 (the preset's 128 x 128 would pad every weight of the tiny model)."""
     import copy
 
     cfg = copy.deepcopy(getattr(mtq, EXPORT_CASES[name]))
@@ -646,6 +649,8 @@ def export_cfg(name):
             first = c[0] if isinstance(c, list) else c
             if first.get("num_bits") == 4:
                 first["block_sizes"] = {-1: 32, "type": "static"}
+            if first.get("num_bits") == (4, 3) and -2 in (first.get("block_sizes") or {}):
+                first["block_sizes"] = {-1: 32, -2: 32}
     return cfg
 
 

@@ -49,6 +49,8 @@ def _cfg(mtq, preset):
             first = c[0] if isinstance(c, list) else c
             if first.get("num_bits") == 4:
                 first["block_sizes"] = {-1: 32, "type": "static"}
+            if first.get("num_bits") == (4, 3) and -2 in (first.get("block_sizes") or {}):
+                first["block_sizes"] = {-1: 32, -2: 32}  # as make_golden.export_cfg
     return cfg
 
 
@@ -83,3 +85,34 @@ def test_export_matches_reference(gpu, case, tmp_path):
     cq = json.loads((tmp_path / "config.json").read_text())["quantization_config"]
     cq["producer"]["version"] = None
     assert cq == META[case]["quantization_config"]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("shape,block", [((256, 512), (128, 128)), ((200, 136), (64, 32)), ((64, 128), (32, 32)),
+                                         ((1000, 1032), (128, 128))])
+@pytest.mark.parametrize("scale_dtype", ["fp32", "own"])
+def test_fp8_block2d_packer_matches_torch(gpu, dtype, shape, block, scale_dtype):
+    """export_fp8_block2d (the FP8_PB_WO packer) against the reference expression
+    (qtensor/fp8_tensor.py:60-117: pad, repeat_interleave the block scales, divide, cast) on the same
+    device tensors: ragged edges, fp32 scales (fp32 quotient) and scales in the weight's own dtype
+    (the quotient rounded to it), NaN / inf / overflowing elements."""
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    g = torch.Generator(device=gpu).manual_seed(31)
+    w = (torch.randn(shape, device=gpu, generator=g) * 3).to(dtype)
+    w.view(-1)[7] = float("nan")
+    w.view(-1)[11] = float("inf")
+    w.view(-1)[13] = -1e4 if dtype != torch.float16 else -6e4  # overflows its block's scale
+    br, bc = block
+    nrb, ncb = -(-shape[0] // br), -(-shape[1] // bc)
+    s = torch.rand(nrb, ncb, device=gpu, generator=g) * 0.02 + 1e-3
+    if scale_dtype == "own":
+        s = s.to(dtype)
+    got = ops.export_fp8_block2d(w, s, br, bc)
+    pad = torch.nn.functional.pad(w, (0, ncb * bc - shape[1], 0, nrb * br - shape[0]))
+    exp = s.repeat_interleave(br, 0).repeat_interleave(bc, 1)
+    want = (pad / exp).to(torch.float8_e4m3fn)[: shape[0], : shape[1]]
+    gb, wb = got.view(torch.uint8), want.view(torch.uint8)
+    nan = torch.isnan(got.float()) & torch.isnan(want.float())  # torch's NaN sign may differ (see exhaustive)
+    assert bool(((gb == wb) | nan).all()), int((~((gb == wb) | nan)).sum())
