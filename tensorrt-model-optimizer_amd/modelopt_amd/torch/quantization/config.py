@@ -572,6 +572,91 @@ MXFP4_MLP_WEIGHT_ONLY_CFG: dict[str, Any] = {
     "algorithm": None,
 }
 
+_NVFP4_B32 = {"num_bits": (2, 1), "block_sizes": {-1: 32, "type": "dynamic", "scale_bits": (4, 3)}}
+W4A16_NVFP4_CFG: dict[str, Any] = _preset(_NVFP4, "keep")
+W4A8_NVFP4_FP8_CFG: dict[str, Any] = _preset(_NVFP4_B32, {"num_bits": (4, 3), "axis": None})
+
+
+def _patterned(names, cfg, extra_disabled=(), base_entries=()) -> dict[str, Any]:
+    """base_disable_all + ``names`` x (weight, input) with ``cfg`` (or the given entries) +
+    default_disabled_quantizers + extra disables: the layout of the reference's pattern presets."""
+    qc = list(_BASE_DISABLE_ALL) + list(base_entries)
+    for n in names:
+        qc += [{"quantizer_name": n + "weight_quantizer", "cfg": cfg}, {"quantizer_name": n + "input_quantizer", "cfg": cfg}]
+    qc += _DEFAULT_DISABLED_QUANTIZERS
+    qc += [{"quantizer_name": n, "enable": False} for n in extra_disabled]
+    return {"quant_cfg": copy.deepcopy(qc), "algorithm": "max"}
+
+
+_MLP_PATTERNS = ["*mlp*", "*.mixer.up_proj.", "*.mixer.down_proj.", "*block_sparse_moe*", "*.experts.*"]
+NVFP4_MLP_ONLY_CFG: dict[str, Any] = _patterned(_MLP_PATTERNS, _NVFP4)
+NVFP4_OMLP_ONLY_CFG: dict[str, Any] = _patterned(["*o_proj*"] + _MLP_PATTERNS[:4], _NVFP4)
+NVFP4_EXPERTS_ONLY_CFG: dict[str, Any] = _patterned(["*block_sparse_moe*", "*.experts.*"], _NVFP4)
+NVFP4_MLP_WEIGHT_ONLY_CFG: dict[str, Any] = {
+    "quant_cfg": copy.deepcopy(
+        _BASE_DISABLE_ALL
+        + [{"quantizer_name": "*mlp*weight_quantizer", "cfg": _NVFP4_B32},
+           {"quantizer_name": "*block_sparse_moe*weight_quantizer", "cfg": _NVFP4_B32}]
+        + _DEFAULT_DISABLED_QUANTIZERS
+    ),
+    "algorithm": "max",
+}
+_MAMBA_MOE_AGGRESSIVE_OFF = ["*fc1_latent_proj*", "*fc2_latent_proj*", "*q_proj*", "*k_proj*", "*v_proj*",
+                             "*o_proj*", "*self_attention.linear_qkv*", "*self_attention.linear_proj*"]
+_MAMBA_MOE_CONSERVATIVE_OFF = _MAMBA_MOE_AGGRESSIVE_OFF + ["*mixer.in_proj*", "*mixer.out_proj*"]
+
+
+def _mamba_moe(fmt, off) -> dict[str, Any]:
+    c = _preset(fmt, fmt)
+    c["quant_cfg"] += [{"quantizer_name": n, "enable": False} for n in off]
+    return c
+
+
+MAMBA_MOE_FP8_AGGRESSIVE_CFG: dict[str, Any] = _mamba_moe(_FP8_PT, _MAMBA_MOE_AGGRESSIVE_OFF)
+MAMBA_MOE_FP8_CONSERVATIVE_CFG: dict[str, Any] = _mamba_moe(_FP8_PT, _MAMBA_MOE_CONSERVATIVE_OFF)
+MAMBA_MOE_NVFP4_AGGRESSIVE_CFG: dict[str, Any] = _mamba_moe(_NVFP4, _MAMBA_MOE_AGGRESSIVE_OFF)
+MAMBA_MOE_NVFP4_CONSERVATIVE_CFG: dict[str, Any] = _mamba_moe(_NVFP4, _MAMBA_MOE_CONSERVATIVE_OFF)
+NVFP4_FOUR_OVER_SIX_CFG: dict[str, Any] = _preset(
+    {"num_bits": (2, 1), "block_sizes": {-1: 16, "type": "static", "scale_bits": (4, 3), "four_over_six": 1}},
+    _NVFP4,
+    {"method": "mse", "fp8_scale_sweep": False, "start_multiplier": 1.0, "stop_multiplier": 1.5, "step_size": 0.5},
+)
+
+# Presets of algorithms / attributes outside this build's scope (DESIGN §8): defined so that code
+# importing them keeps working; mtq.quantize raises NotImplementedError for smoothquant / svdquant /
+# local_hessian (algorithm_config) and for rotated quantizers (TensorQuantizer).
+INT8_SMOOTHQUANT_CFG: dict[str, Any] = _preset({"num_bits": 8, "axis": 0}, {"num_bits": 8, "axis": None},
+                                               "smoothquant")
+NVFP4_SVDQUANT_DEFAULT_CFG: dict[str, Any] = _preset(_NVFP4, _NVFP4, {"method": "svdquant", "lowrank": 32})
+NVFP4_W4A4_WEIGHT_LOCAL_HESSIAN_CFG: dict[str, Any] = _preset(
+    _NVFP4_STATIC, _NVFP4, {"method": "local_hessian", "fp8_scale_sweep": True}
+)
+NVFP4_KV_ROTATE_CFG: dict[str, Any] = {
+    "quant_cfg": [
+        {"quantizer_name": "*q_bmm_quantizer", "cfg": {"rotate": True}, "enable": False},
+        {"quantizer_name": "*k_bmm_quantizer", "cfg": {**copy.deepcopy(_NVFP4), "rotate": True}},
+        {"quantizer_name": "*v_bmm_quantizer", "cfg": copy.deepcopy(_NVFP4)},
+    ],
+    "algorithm": "max",
+}
+
+__all__ += [
+    "W4A16_NVFP4_CFG",
+    "W4A8_NVFP4_FP8_CFG",
+    "NVFP4_MLP_ONLY_CFG",
+    "NVFP4_OMLP_ONLY_CFG",
+    "NVFP4_EXPERTS_ONLY_CFG",
+    "NVFP4_MLP_WEIGHT_ONLY_CFG",
+    "MAMBA_MOE_FP8_AGGRESSIVE_CFG",
+    "MAMBA_MOE_FP8_CONSERVATIVE_CFG",
+    "MAMBA_MOE_NVFP4_AGGRESSIVE_CFG",
+    "MAMBA_MOE_NVFP4_CONSERVATIVE_CFG",
+    "NVFP4_FOUR_OVER_SIX_CFG",
+    "INT8_SMOOTHQUANT_CFG",
+    "NVFP4_SVDQUANT_DEFAULT_CFG",
+    "NVFP4_W4A4_WEIGHT_LOCAL_HESSIAN_CFG",
+    "NVFP4_KV_ROTATE_CFG",
+]
 __all__ += [
     "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG",
     "FP8_DEFAULT_CFG",

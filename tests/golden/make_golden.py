@@ -938,6 +938,11 @@ def gen_presets():
         "W4A8_MXFP4_FP8_CFG", "MXFP4_MLP_WEIGHT_ONLY_CFG", "NVFP4_DEFAULT_CFG", "NVFP4_AWQ_LITE_CFG",
         "W4A8_AWQ_BETA_CFG", "FP8_KV_CFG", "NVFP4_KV_CFG", "NVFP4_AWQ_CLIP_CFG", "NVFP4_AWQ_FULL_CFG",
         "NVFP4_W4A4_WEIGHT_MSE_FP8_SWEEP_CFG", "FP8_AFFINE_KV_CFG", "NVFP4_AFFINE_KV_CFG", "NVFP4_FP8_MHA_CONFIG",
+        "W4A16_NVFP4_CFG", "W4A8_NVFP4_FP8_CFG", "NVFP4_MLP_ONLY_CFG", "NVFP4_OMLP_ONLY_CFG", "NVFP4_EXPERTS_ONLY_CFG",
+        "NVFP4_MLP_WEIGHT_ONLY_CFG", "MAMBA_MOE_FP8_AGGRESSIVE_CFG", "MAMBA_MOE_FP8_CONSERVATIVE_CFG",
+        "MAMBA_MOE_NVFP4_AGGRESSIVE_CFG", "MAMBA_MOE_NVFP4_CONSERVATIVE_CFG", "NVFP4_FOUR_OVER_SIX_CFG",
+        "INT8_SMOOTHQUANT_CFG", "NVFP4_SVDQUANT_DEFAULT_CFG", "NVFP4_W4A4_WEIGHT_LOCAL_HESSIAN_CFG",
+        "NVFP4_KV_ROTATE_CFG",
     ]
 
     def enc(o):

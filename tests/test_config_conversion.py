@@ -179,3 +179,22 @@ def test_max_calibrator_skips_same_view():
     with torch.no_grad():
         p.mul_(2)
     assert not c._same_as_last(p[2])  # version bumped
+
+
+@pytest.mark.parametrize("name", ["INT8_SMOOTHQUANT_CFG", "NVFP4_SVDQUANT_DEFAULT_CFG",
+                                  "NVFP4_W4A4_WEIGHT_LOCAL_HESSIAN_CFG"])
+def test_out_of_scope_presets_raise(name):
+    """Presets of algorithms outside the MI355X path exist (import compatibility) and raise
+    NotImplementedError when used, before any calibration work."""
+    import torch
+    import torch.nn as nn
+
+    with pytest.raises(NotImplementedError):
+        mtq.quantize(nn.Linear(16, 16), getattr(mtq, name), lambda m: m(torch.randn(2, 16)))
+
+
+def test_rotated_kv_preset_raises():
+    from modelopt_amd.torch.quantization.nn.modules.tensor_quantizer import TensorQuantizer
+
+    with pytest.raises(NotImplementedError):
+        TensorQuantizer(QuantizerAttributeConfig(**mtq.NVFP4_KV_ROTATE_CFG["quant_cfg"][1]["cfg"]))
