@@ -634,6 +634,10 @@ EXPORT_CASES = {
     "mxfp4": "MXFP4_DEFAULT_CFG",
     "mxfp8": "MXFP8_DEFAULT_CFG",
     "fp8_pb_wo": "FP8_2D_BLOCKWISE_WEIGHT_ONLY_CFG",
+    "int8_wo": "INT8_WEIGHT_ONLY_CFG",
+    "w4a16_nvfp4": "W4A16_NVFP4_CFG",
+    "w4a8_nvfp4_fp8": "W4A8_NVFP4_FP8_CFG",
+    "w4a8_mxfp4_fp8": "W4A8_MXFP4_FP8_CFG",
 }
 
 
