@@ -29,3 +29,4 @@ from .nn.modules.tensor_quantizer import (
 )
 from . import qtensor
 from .compress import CompressConfig, RealQuantLinear, compress, is_real_quantized
+from .utils.core_utils import update_quant_cfg_with_kv_cache_quant

@@ -21,7 +21,10 @@ __all__ = [
     "AWQClipCalibConfig",
     "AWQFullCalibConfig",
     "AWQLiteCalibConfig",
+    "LayerwiseConfig",
     "MaxCalibConfig",
+    "MseCalibConfig",
+    "find_quant_cfg_entry_by_path",
     "QuantizeAlgorithmConfig",
     "QuantizeConfig",
     "QuantizerAttributeConfig",
@@ -324,6 +327,30 @@ def _legacy_entry(name, v, parent_class=None):
             e["enable"] = v.pop("enable")
         e["cfg"] = v
     return e
+
+
+def find_quant_cfg_entry_by_path(quant_cfg_list, quantizer_name: str):
+    """The LAST entry of a ``quant_cfg`` list whose ``quantizer_name`` equals ``quantizer_name``
+    exactly (no wildcard matching; later entries override earlier ones, so the last one is the
+    effective configuration) -- reference config.py:245-276.  KeyError when there is none."""
+    found = None
+    for entry in quant_cfg_list:
+        if entry.get("quantizer_name") == quantizer_name:
+            found = entry
+    if found is None:
+        raise KeyError(f"No quant_cfg entry with quantizer_name={quantizer_name!r}")
+    return found
+
+
+class LayerwiseConfig(_Config):
+    """Layer-by-layer calibration options (reference config.py:712-770; ``algorithm["layerwise"]``,
+    run by ``layerwise.layerwise_calibrate``)."""
+
+    enable: bool = False
+    get_qdq_activations_from_prev_layer: bool = False
+    checkpoint_dir: str | None = None
+    save_every: int = Field(default=1, ge=1)
+    calib_mutates_weights: bool = True
 
 
 class QuantizeAlgorithmConfig(_Config):

@@ -18,6 +18,7 @@ from .utils.names import is_quantized
 
 __all__ = [
     "convert_to_quantized_model",
+    "preserve_quantizer_attributes_context",
     "quantizer_state",
     "register",
     "replace_quant_module",
@@ -257,3 +258,41 @@ def unregister(original_cls: nn.Module):
 
 
 ReplaceFilter = Callable[[str], bool]
+
+
+@contextlib.contextmanager
+def preserve_quantizer_attributes_context(quant_model: nn.Module):
+    """Restore every quantizer's properties (``get_modelopt_state(properties_only=True)``) and its
+    TensorQuantizer / SequentialQuantizer type on exit -- parameters, buffers and calibrators are
+    not copied (reference conversion.py:507-567).  A quantizer that a cfg change inside swapped
+    for the other type is rebuilt in its original type first."""
+    saved: dict[str, tuple] = {}
+    for name, m in quant_model.named_modules():
+        if isinstance(m, SequentialQuantizer):
+            saved[name] = (SequentialQuantizer, [q.get_modelopt_state(properties_only=True) for q in m])
+        elif isinstance(m, TensorQuantizer):
+            saved[name] = (TensorQuantizer, m.get_modelopt_state(properties_only=True))
+    try:
+        yield
+    finally:
+        for name, m in list(quant_model.named_modules()):
+            if name not in saved:
+                continue
+            kind, state = saved[name]
+            parent_name, _, attr = name.rpartition(".")
+            parent = quant_model.get_submodule(parent_name) if parent_name else quant_model
+            if kind is SequentialQuantizer and not isinstance(m, SequentialQuantizer):
+                m = SequentialQuantizer(*(TensorQuantizer() for _ in state))
+                setattr(parent, attr, m)
+                for q, st in zip(m, state):
+                    q.set_from_modelopt_state(st, properties_only=True)
+            elif kind is TensorQuantizer and not isinstance(m, TensorQuantizer):
+                m = TensorQuantizer()
+                setattr(parent, attr, m)
+                m.set_from_modelopt_state(state, properties_only=True)
+            elif kind is TensorQuantizer:
+                m.set_from_modelopt_state(state, properties_only=True)
+            else:  # still a SequentialQuantizer
+                for q, st in zip(m, state):
+                    q.set_from_modelopt_state(st, properties_only=True)
+

@@ -10,6 +10,7 @@ the model when it is saved.
 
 from __future__ import annotations
 
+import contextlib
 import fnmatch
 import inspect
 import warnings
@@ -30,6 +31,8 @@ from .utils.names import is_quantized
 
 __all__ = [
     "calibrate",
+    "compute_quantization_mse",
+    "temporarily_fold_weights",
     "disable_quantizer",
     "enable_quantizer",
     "fold_weight",
@@ -199,3 +202,74 @@ def fold_weight(model: nn.Module, keep_attrs: bool = False):
     for _, module in model.named_modules():
         if isinstance(module, QuantModule):
             module.fold_weight(keep_attrs)
+
+
+@contextlib.contextmanager
+def temporarily_fold_weights(model: nn.Module, snapshot_device: torch.device | str | None = None):
+    """Fold the fake-quant weights for a frozen inference region, restoring them on exit
+    (reference model_quant.py:740-806): each QuantModule's ``fold_weight(keep_attrs=True)``, the
+    quantizers' properties restored by ``preserve_quantizer_attributes_context``, and every
+    weight a quantization / pre_quant_scale / rotation changes copied back in place from a
+    snapshot (on ``snapshot_device``, default the weight's own), exceptions included.
+    SequentialQuantizer weights are not supported (NotImplementedError), as in the reference."""
+    from .conversion import preserve_quantizer_attributes_context
+
+    pairs = []
+    for module in model.modules():
+        if not isinstance(module, QuantModule):
+            continue
+        for weight, q in module.iter_weights_for_calibration():
+            if not isinstance(weight, torch.Tensor):
+                continue
+            if isinstance(q, SequentialQuantizer):
+                raise NotImplementedError("temporarily_fold_weights does not support SequentialQuantizer")
+            if not isinstance(q, TensorQuantizer) or not q.fake_quant:
+                continue
+            pairs.append((weight.to_local() if hasattr(weight, "to_local") else weight, q))
+    snapshots = {}
+    for w, q in pairs:
+        if q.is_enabled or q.pre_quant_scale is not None or q.rotate_is_enabled:
+            if id(w) not in snapshots:
+                snapshots[id(w)] = (w, w.detach().clone() if snapshot_device is None
+                                    else w.detach().to(snapshot_device, copy=True))
+    with preserve_quantizer_attributes_context(model):
+        try:
+            fold_weight(model, keep_attrs=True)
+            yield
+        finally:
+            with torch.no_grad():
+                for w, snap in snapshots.values():
+                    w.copy_(snap)
+
+
+@torch.no_grad()
+def compute_quantization_mse(model: nn.Module, forward_loop, wildcards="*") -> dict[str, float]:
+    """Mean over the ``forward_loop`` batches of mean((x - qdq(x))^2) for every enabled fake-quant
+    TensorQuantizer whose name matches ``wildcards`` (fnmatch patterns or callables; reference
+    model_quant.py:809-882); disabled / non-fake quantizers are absent from the result."""
+    pats = wildcards if isinstance(wildcards, list) else [wildcards]
+
+    def match(name):
+        return any(fnmatch.fnmatch(name, w) if isinstance(w, str) else w(name) for w in pats)
+
+    acc: dict[str, list] = {}
+    hooks = []
+    for name, m in model.named_modules():
+        if not isinstance(m, TensorQuantizer) or not match(name):
+            continue
+        if not (m._if_quant and m._fake_quant) or m._disabled:
+            continue
+        acc[name] = [0.0, 0]
+
+        def hook(mod, inp, out, a=acc[name]):
+            a[0] += torch.mean((inp[0].detach().float() - out.detach().float()) ** 2).item()
+            a[1] += 1
+
+        hooks.append(m.register_forward_hook(hook))
+    try:
+        forward_loop(model)
+    finally:
+        for h in hooks:
+            h.remove()
+    return {n: s / c for n, (s, c) in acc.items() if c > 0}
+

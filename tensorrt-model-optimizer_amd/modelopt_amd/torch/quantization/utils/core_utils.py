@@ -182,3 +182,18 @@ def gc_paused():
     finally:
         if was:
             gc.enable()
+
+
+def update_quant_cfg_with_kv_cache_quant(quant_cfg: dict, kv_cache_quant_cfg: list) -> dict:
+    """A deep copy of ``quant_cfg`` with the KV-cache entries (e.g. ``FP8_KV_CFG["quant_cfg"]``)
+    appended to its ``quant_cfg`` list -- an empty / missing list starts from "disable every
+    quantizer" -- and ``algorithm`` defaulted to ``"max"`` (reference utils/core_utils.py:1049-1075)."""
+    import copy as _copy
+
+    out = _copy.deepcopy(quant_cfg)
+    inner = out.get("quant_cfg") or [{"quantizer_name": "*", "enable": False}]
+    out["quant_cfg"] = list(inner) + _copy.deepcopy(list(kv_cache_quant_cfg))
+    if not out.get("algorithm"):
+        out["algorithm"] = "max"
+    return out
+
