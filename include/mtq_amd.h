@@ -172,17 +172,19 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
 /* torch.histc's CPU accumulation for calls above 2^24 elements (calib/histogram.py:116-130 ->
  * torch.histc -> at::parallel_for): element chunk c is [bounds[c], bounds[c+1]) (device int64
  * [chunks + 1], e.g. the skip_zeros boundaries mapped back to the input), or, with bounds null,
- * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  Two launches: each chunk is counted exactly
- * into its row of `scratch` (uint32 [chunks * bins]: ALL ZERO on entry, left all zero on return --
- * keep one per stream and reuse it), then hist[b] = sum_c min(fp32(scratch[c][b]), 2^24) in chunk
- * order, + accum[b] for b < accum_n (the calibrator's running histogram, calib/histogram.py:127;
- * accum may alias hist; accum_n 0 = none) (fp32 [bins], overwritten).
+ * [c * chunk_elems, min((c + 1) * chunk_elems, n)).  Two launches: the chunks are counted exactly
+ * by a fixed number of workgroups each, every workgroup storing its bin row into `scratch` (uint32
+ * [scratch_words >= mtq_histogram_chunked_scratch_words(n, chunks, bins)], contents irrelevant,
+ * overwritten), then hist[b] = sum_c min(fp32(count_c[b]), 2^24) in chunk order, + accum[b] for
+ * b < accum_n (the calibrator's running histogram, calib/histogram.py:127; accum may alias hist;
+ * accum_n 0 = none) (fp32 [bins], overwritten).
  * bf16 / f16 only, x 16-byte aligned, n % 8 == 0, bins <= 8192 (MTQ_ERR_DTYPE /
  * MTQ_ERR_INVALID_ARG otherwise: the caller counts chunk by chunk with mtq_histogram_abs). */
+int64_t mtq_histogram_chunked_scratch_words(int64_t n, int chunks, int bins);
 int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                               int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
-                              uint32_t *scratch, const float *accum, int64_t accum_n, float *hist,
-                              hipStream_t stream);
+                              uint32_t *scratch, int64_t scratch_words, const float *accum, int64_t accum_n,
+                              float *hist, hipStream_t stream);
 
 /* The skip_zeros chunk boundaries of the call above, computed on the device (no host sync):
  * torch.histc counts the N non-zero elements as at::parallel_for chunks -- T' = min(threads,

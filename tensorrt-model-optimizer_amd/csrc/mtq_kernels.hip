@@ -1435,50 +1435,77 @@ __global__ __launch_bounds__(kHistDivThreads) void hist_div_kernel(
 constexpr int kHistValThreads = 1024;
 constexpr int kHistPatterns = 32768;
 //
-// CHUNKED: the torch.histc chunk emulation in one launch.  Chunk c covers elements [e0, e1) (from
-// `bounds`, or c * chunk_elems clipped to n_elems when bounds is null) and owns `bpc` consecutive
-// blocks and the count row counts[c * bins, +bins); element bounds need not fall on vectors, so
-// the two edge vectors of a chunk mask their out-of-chunk halves to the dropped NaN pattern.
+// CHUNKED: the torch.histc chunk emulation.  Chunk c covers elements [e0, e1) (from `bounds`, or
+// c * chunk_elems clipped to n_elems when bounds is null) and owns `bpc` consecutive workgroups;
+// each workgroup stores its whole LDS bin row (plain non-temporal stores, no atomics) into its own
+// row of the scratch, rows[block * bins, +bins); element bounds need not fall on vectors, so the
+// two edge vectors of a chunk are counted separately (below).
 //
-// The rows are folded by a second, small launch (hist_fold_rows_kernel): hist[b] = sum_c
-// min(fp32(row_c[b]), 2^24) in chunk order (+ an optional running histogram), zeroing the rows
-// again -- the scratch is all zero between calls, so no memset is needed.  (r05: the fold in the
-// counting launch -- each workgroup waiting for its row atomics, an agent-scope check-in counter,
-// the last workgroup exchanging 32 K words -- cost 12 us at the launch's tail against 5.5 us for
-// the second launch; bf16 [8192, 14336], 16 chunks, 2048 bins.)
+// The rows are folded by a second, small launch (hist_fold_blocks_kernel): chunk c's count of bin
+// b is the exact sum of its bpc workgroup rows, and hist[b] = sum_c min(fp32(count_c[b]), 2^24)
+// in chunk order (+ an optional running histogram).  Every row is overwritten by every call, so
+// the scratch needs no zeroing.  (r05: per-chunk rows filled by workgroup atomics and zeroed again
+// by the fold measured 42.4 us against 41.0 us for this form, count + fold, bf16 [8192, 14336],
+// 16 chunks, scripts/exp/hist_exp.hip; a fold inside the counting launch -- its last workgroup
+// after an agent-scope check-in -- cost 12 us at the launch's tail.)
 struct HistChunks {
   const int64_t *bounds;  // [chunks + 1] element offsets (device), or null: uniform chunks
   int64_t chunk_elems;
   int64_t n_elems;
-  int bpc;  // blocks per chunk
+  int bpc;  // workgroups per chunk
   int chunks;
-  uint32_t *rows;  // [chunks, bins] counts; zero on entry, zeroed again by the fold launch
+  uint32_t *rows;  // [chunks * bpc, bins] per-workgroup counts, overwritten
 };
 
-// hist[b] = sum_c min(fp32(rows[c][b]), 2^24) in chunk order (torch.histc's thread-order fold of
-// its fp32 per-thread counts), then + accum[b] for b < accum_n (the calibrator's running
-// histogram, `hist[:old.numel()] += old`), rows zeroed.  16 chunks' loads in flight per lane.
-__global__ __launch_bounds__(256) void hist_fold_rows_kernel(uint32_t *__restrict__ rows, int chunks, int bins,
-                                                             const float *accum, int64_t accum_n,
-                                                             float *hist) {  // accum may alias hist
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= bins) return;
-  float h = 0.f;
-  for (int c0 = 0; c0 < chunks; c0 += 16) {
-    uint32_t v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = c0 + j < chunks ? rows[(int64_t)(c0 + j) * bins + b] : 0u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      h += fminf((float)v[j], 16777216.f);  // + 0 past the last chunk
-      if (c0 + j < chunks) rows[(int64_t)(c0 + j) * bins + b] = 0u;
-    }
-  }
-  if (b < accum_n) h += accum[b];
-  hist[b] = h;
+// workgroups per chunk of the chunked count: ~one 1024-thread workgroup per CU in total, at
+// least kHistValThreads * 8 vectors each
+int64_t hist_chunk_bpc(int64_t n, int chunks) {
+  const int64_t cvec = (n / 8 + chunks - 1) / chunks;
+  int64_t bpc = ((int64_t)num_cus() + chunks - 1) / chunks;
+  const int64_t by_size = (cvec + (int64_t)kHistValThreads * 8 - 1) / ((int64_t)kHistValThreads * 8);
+  bpc = bpc < by_size ? bpc : by_size;
+  return bpc < 1 ? 1 : bpc;
 }
 
-template <typename T, int U, bool PF, bool CHUNKED = false>
+// 1024 threads = 64 bins x 16 chunk lanes: a thread sums its chunk's bpc workgroup rows (exact,
+// uint32), clamps at 2^24 in fp32; the chunk-0 lane of each bin adds the 16 clamped counts of the
+// group in chunk order (torch.histc's thread-order fold of its fp32 per-thread counts), group
+// after group, then + accum[b] for b < accum_n (the calibrator's running histogram,
+// `hist[:old.numel()] += old`).
+__global__ __launch_bounds__(1024) void hist_fold_blocks_kernel(const uint32_t *__restrict__ rows, int bpc,
+                                                                int chunks, int bins, const float *accum,
+                                                                int64_t accum_n, float *hist) {  // accum may alias hist
+  __shared__ float part[16][64];
+  const int bl = threadIdx.x & 63, cl = threadIdx.x >> 6, b = blockIdx.x * 64 + bl;
+  float h = 0.f;
+  for (int c0 = 0; c0 < chunks; c0 += 16) {
+    const int c = c0 + cl;
+    if (c < chunks && b < bins) {
+      const uint32_t *r = rows + (int64_t)c * bpc * bins + b;
+      uint32_t sum = 0;
+      for (int k0 = 0; k0 < bpc; k0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = k0 + k < bpc ? __builtin_nontemporal_load(r + (int64_t)(k0 + k) * bins) : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += v[k];
+      }
+      part[cl][bl] = fminf((float)sum, 16777216.f);
+    }
+    __syncthreads();
+    if (cl == 0 && b < bins) {
+      const int m = chunks - c0 < 16 ? chunks - c0 : 16;
+      for (int k = 0; k < m; ++k) h += part[k][bl];
+    }
+    __syncthreads();
+  }
+  if (cl == 0 && b < bins) {
+    if (b < accum_n) h += accum[b];
+    hist[b] = h;
+  }
+}
+
+template <typename T, int U, bool CHUNKED = false>
 __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
     const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
     int skip_zeros, uint32_t *counts, HistChunks ch) {
@@ -1486,33 +1513,9 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
   uint32_t *vh = sh;                  // [32768] counts per |x| bit pattern
   uint32_t *bh = sh + kHistPatterns;  // [bins]
-  float lo = 0.f, hi = *hmax;
-  if (hi == lo) {
-    lo -= 1.f;
-    hi += 1.f;
-  }
-  // Only patterns p <= phi, the largest pattern whose value is <= hi, can land in a bin (the
-  // patterns of non-negative floats are ordered as their values; NaN hi: none), so only those
-  // counters are zeroed here and folded below; the count loop still increments every pattern, the
-  // entries past phi are never read.  bf16 [32768, 4096] with |x| <= 96: 128 -> 68 KiB zeroed and
-  // folded per block (r04: fixed cost 5.1 us of the 46.6 us launch, scripts/exp/hist_exp.hip).
-  int phi;
-  if (!(hi >= 0.f)) {
-    phi = -1;
-  } else if constexpr (__is_same(T, __bf16)) {
-    const uint32_t b = __float_as_uint(hi) >> 16;  // truncation = round toward zero
-    phi = (int)(b < 0x7F80u ? b : 0x7F80u);
-  } else {
-    // round toward zero to f16 (v_cvt_pkrtz_f16_f32): the largest f16 <= hi (65504 above it)
-    const auto h2 = __builtin_amdgcn_cvt_pkrtz(hi, 0.f);
-    uint16_t hb;
-    __builtin_memcpy(&hb, &h2, 2);
-    phi = (int)(hb < 0x7C00u ? hb : 0x7C00u);
-  }
-  const int nz4 = (phi + 4) / 4;  // 16-byte words covering patterns [0, phi]
-  for (int i = threadIdx.x; i < nz4; i += kHistValThreads)
-    reinterpret_cast<uint4 *>(vh)[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (int b = threadIdx.x; b < bins; b += kHistValThreads) bh[b] = 0;
+  // the workgroup's vector range first, so its first loads are in flight before the hmax round
+  // trip and the LDS zeroing below (r05: 41.8 -> 38.3 us with the A/B loop, bf16 [8192, 14336],
+  // scripts/exp/hist_exp.hip v562)
   int64_t v0, v1, e0 = 0, e1 = 0;
   if constexpr (CHUNKED) {
     const int c = blockIdx.x / ch.bpc, s = blockIdx.x % ch.bpc;
@@ -1534,57 +1537,75 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
     v1 = v0 + per;
     v1 = v1 < cv1 ? v1 : cv1;
     v0 = v0 < v1 ? v0 : v1;
-    counts += (int64_t)c * bins;
   } else {
     v0 = (int64_t)blockIdx.x * vec_per_block;
     v1 = v0 + vec_per_block;
     v1 = v1 < nvec ? v1 : nvec;
   }
+  // Two named register batches (A, B) with unconditional loads clamped to the range's last vector
+  // (vector 0 for an empty range; nvec >= 1): no load sits under a branch and no in-flight
+  // register is copied, so the wait in front of each batch's count is vmcnt(U) -- the other
+  // batch stays in flight -- where the earlier cur / next form, its next-batch load under a
+  // condition, compiled to vmcnt(0) before every count (ISA).  Lanes past the range count a
+  // per-lane NaN pattern (> phi, never folded) so the tail's dummy atomics do not all collide.
+  const int64_t vlast = v1 > 0 ? v1 - 1 : 0;
+  auto ld = [&](int64_t k) -> u32x4 {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + (k < vlast ? k : vlast) * 8));
+  };
+  const uint32_t dummy = 0x7FC0u + (threadIdx.x & 63u);
+  auto count = [&](const u32x4 v, bool ok) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      atomicAdd(vh + (ok ? (w[j] & 0x7FFFu) : dummy), 1u);
+      atomicAdd(vh + (ok ? ((w[j] >> 16) & 0x7FFFu) : dummy), 1u);
+    }
+  };
   constexpr int64_t kStep = (int64_t)kHistValThreads * U;
-  // one U-vector batch per lane; past-the-end slots read as a NaN pattern (dropped by the fold)
-  auto load = [&](int64_t i, uint4 (&v)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t k = i + (int64_t)u * kHistValThreads;
-      if (k < v1) {
-        const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(x + k * 8));
-        v[u] = make_uint4(r.x, r.y, r.z, r.w);
-      } else {
-        v[u] = make_uint4(0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu, 0x7FFF7FFFu);
-      }
-    }
-  };
-  auto count = [&](const uint4 (&v)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        atomicAdd(vh + (w[j] & 0x7FFFu), 1u);
-        atomicAdd(vh + ((w[j] >> 16) & 0x7FFFu), 1u);
-      }
-    }
-  };
   int64_t i = v0 + threadIdx.x;
-  if constexpr (PF) {
-    // register double buffer: the next batch's loads are in flight while this one is counted
-    uint4 cur[U];
-    load(i, cur);
-    __syncthreads();  // LDS zeroed (after the first loads were issued)
-    for (; i < v1; i += kStep) {
-      uint4 nxt[U];
-      if (i + kStep < v1) load(i + kStep, nxt);
-      count(cur);
+  u32x4 a[U], b[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-    }
+  for (int u = 0; u < U; ++u) a[u] = ld(i + (int64_t)u * kHistValThreads);
+
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  // Only patterns p <= phi, the largest pattern whose value is <= hi, can land in a bin (the
+  // patterns of non-negative floats are ordered as their values; NaN hi: none), so only those
+  // counters are zeroed here and folded below; the count loop still increments every pattern, the
+  // entries past phi are never read.  bf16 [32768, 4096] with |x| <= 96: 128 -> 68 KiB zeroed and
+  // folded per block (r04: fixed cost 5.1 us of the 46.6 us launch, scripts/exp/hist_exp.hip).
+  int phi;
+  if (!(hi >= 0.f)) {
+    phi = -1;
+  } else if constexpr (__is_same(T, __bf16)) {
+    const uint32_t hb = __float_as_uint(hi) >> 16;  // truncation = round toward zero
+    phi = (int)(hb < 0x7F80u ? hb : 0x7F80u);
   } else {
-    __syncthreads();
-    for (; i < v1; i += kStep) {
-      uint4 v[U];
-      load(i, v);
-      count(v);
-    }
+    // round toward zero to f16 (v_cvt_pkrtz_f16_f32): the largest f16 <= hi (65504 above it)
+    const auto h2 = __builtin_amdgcn_cvt_pkrtz(hi, 0.f);
+    uint16_t hb;
+    __builtin_memcpy(&hb, &h2, 2);
+    phi = (int)(hb < 0x7C00u ? hb : 0x7C00u);
+  }
+  const int nz4 = (phi + 4) / 4;  // 16-byte words covering patterns [0, phi]
+  for (int k = threadIdx.x; k < nz4; k += kHistValThreads)
+    reinterpret_cast<uint4 *>(vh)[k] = make_uint4(0u, 0u, 0u, 0u);
+  for (int k = threadIdx.x; k < bins; k += kHistValThreads) bh[k] = 0;
+  __syncthreads();  // LDS zeroed (the first batch's loads issued before)
+  // (no branch around B's count either: with one, the compiler sank B's loads into it and waited
+  // vmcnt(0) right behind them; a past-the-end B batch costs its lanes' dummy atomics instead)
+  for (; i < v1; i += 2 * kStep) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ld(i + kStep + (int64_t)u * kHistValThreads);
+#pragma unroll
+    for (int u = 0; u < U; ++u) count(a[u], i + (int64_t)u * kHistValThreads < v1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = ld(i + 2 * kStep + (int64_t)u * kHistValThreads);
+#pragma unroll
+    for (int u = 0; u < U; ++u) count(b[u], i + kStep + (int64_t)u * kHistValThreads < v1);
   }
   if constexpr (CHUNKED) {
     if (blockIdx.x % ch.bpc == 0 && threadIdx.x == 0 && e1 > e0) {
@@ -1640,8 +1661,13 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
     if (run_c) atomicAdd(bh + run_b, run_c);
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < bins; b += kHistValThreads)
-    if (bh[b]) atomicAdd(counts + b, bh[b]);
+  if constexpr (CHUNKED) {
+    uint32_t *row = ch.rows + (int64_t)blockIdx.x * bins;
+    for (int b = threadIdx.x; b < bins; b += kHistValThreads) __builtin_nontemporal_store(bh[b], row + b);
+  } else {
+    for (int b = threadIdx.x; b < bins; b += kHistValThreads)
+      if (bh[b]) atomicAdd(counts + b, bh[b]);
+  }
 }
 
 // skip_zeros chunk boundaries on the device (replaces an int64 cumsum over the whole input, a
@@ -2761,18 +2787,34 @@ __global__ __launch_bounds__(kThreads) void export_fp8_vec_kernel(const T *__res
 // the FP8_PB_WO export, export/quant_utils.py:874-877): vector i (N elements along a row, never
 // across a column block: bc % N == 0) uses scale[(row / br) * ncb + col / bc] of the fp32 block
 // grid; the fp32 quotient (input / expanded_scales promotes to fp32) converted as the per-row path.
-template <typename T>
+// U vectors per lane, all loaded before the first scale index is formed (the one-vector form
+// with three int64 divisions per vector ran at 0.62 of the roofline, r05); row / block indices
+// from 32-bit multiply-high dividers when every index fits (IDX32).
+template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_fp8_blk2d_kernel(const T *__restrict__ x, uint8_t *__restrict__ y,
-                                                                    int64_t nvec, int64_t cv, int64_t br, int64_t bcv,
-                                                                    int64_t ncb, const float *__restrict__ scale,
-                                                                    int round_dtype, int native) {
+                                                                    int64_t nvec, int64_t cv, FastDiv fcv, int64_t br,
+                                                                    FastDiv fbr, int64_t bcv, FastDiv fbcv, int64_t ncb,
+                                                                    const float *__restrict__ scale, int round_dtype,
+                                                                    int native) {
   constexpr int N = Vec<T>::N;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= nvec) return;
-  const Vec<T> v = ldg_vec_nt(x + i * N);
-  const int64_t row = i / cv, cvec = i - row * cv;
-  const float s = scale[(row / br) * ncb + cvec / bcv];
-  export_fp8_pack_store<T>(i, v, y, s, round_dtype, native);
+  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  Vec<T> v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: see export_mxfp4_vec_kernel
+    const int64_t i = base + u * kThreads;
+    v[u] = ldg_vec_nt(x + (i < nvec ? i : nvec - 1) * N);
+  }
+  float sv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    int64_t i = base + u * kThreads;
+    i = i < nvec ? i : nvec - 1;
+    const int64_t row = idx_div<IDX32>(i, cv, fcv), cvec = i - row * cv;
+    sv[u] = scale[idx_div<IDX32>(row, br, fbr) * ncb + idx_div<IDX32>(cvec, bcv, fbcv)];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * kThreads < nvec) export_fp8_pack_store<T>(base + u * kThreads, v[u], y, sv[u], round_dtype, native);
 }
 
 template <int U, typename T, bool IDX32>
@@ -3155,7 +3197,7 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
         vpb = vpb < min_per_block ? min_per_block : vpb;
         blocks = (nvec + vpb - 1) / vpb;
         const size_t shr = ((size_t)kHistPatterns + (size_t)bins) * 4;
-        auto kern = hist_value_kernel<T, 2, true>;
+        auto kern = hist_value_kernel<T, 2>;
         static bool attr = false;
         if (!attr) {
           (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -3203,28 +3245,28 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
   });
 }
 
+int64_t mtq_histogram_chunked_scratch_words(int64_t n, int chunks, int bins) {
+  if (n < 0 || chunks < 1 || bins < 1) return -1;
+  return (int64_t)chunks * hist_chunk_bpc(n, chunks) * bins;
+}
+
 int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
                               int skip_zeros, const int64_t *bounds, int64_t chunk_elems, int chunks,
-                              uint32_t *scratch, const float *accum, int64_t accum_n, float *hist,
-                              hipStream_t stream) {
+                              uint32_t *scratch, int64_t scratch_words, const float *accum, int64_t accum_n,
+                              float *hist, hipStream_t stream) {
   if (n < 0 || bins < 1 || bins > 8192 || chunks < 1 || !hmax || !scratch || !hist || (n > 0 && !x))
     return MTQ_ERR_INVALID_ARG;
   if (accum_n < 0 || accum_n > bins || (accum_n > 0 && !accum)) return MTQ_ERR_INVALID_ARG;
   if (!bounds && (chunk_elems < 1 || (chunks - 1) * chunk_elems >= n)) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
   if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
+  const int64_t bpc = hist_chunk_bpc(n, chunks);
+  if ((int64_t)chunks * bpc > INT32_MAX || scratch_words < (int64_t)chunks * bpc * bins) return MTQ_ERR_INVALID_ARG;
   return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
     using T = decltype(t);
     if constexpr (sizeof(T) == 2) {
-      // ~one 1024-thread block per CU in total, at least kHistValThreads * 8 vectors per block
-      const int64_t cvec = (n / 8 + chunks - 1) / chunks;
-      int64_t bpc = ((int64_t)num_cus() + chunks - 1) / chunks;
-      const int64_t by_size = (cvec + (int64_t)kHistValThreads * 8 - 1) / ((int64_t)kHistValThreads * 8);
-      bpc = bpc < by_size ? bpc : by_size;
-      bpc = bpc < 1 ? 1 : bpc;
-      if ((int64_t)chunks * bpc > INT32_MAX) return MTQ_ERR_INVALID_ARG;
       const size_t shr = ((size_t)kHistPatterns + (size_t)bins) * 4;
-      auto kern = hist_value_kernel<T, 2, true, true>;
+      auto kern = hist_value_kernel<T, 2, true>;
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -3234,9 +3276,9 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
       const HistChunks ch{bounds, chunk_elems, n, (int)bpc, chunks, scratch};
       count_dispatch(kDispHistValueChunked);
       kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
-                                                                      hmax, bins, skip_zeros, scratch, ch);
-      hist_fold_rows_kernel<<<(unsigned)((bins + 255) / 256), 256, 0, stream>>>(scratch, chunks, bins, accum,
-                                                                                accum_n, hist);
+                                                                      hmax, bins, skip_zeros, nullptr, ch);
+      hist_fold_blocks_kernel<<<(unsigned)((bins + 63) / 64), 1024, 0, stream>>>(scratch, (int)bpc, chunks, bins,
+                                                                                 accum, accum_n, hist);
       return check_launch();
     }
     return MTQ_ERR_DTYPE;
@@ -3398,10 +3440,18 @@ int mtq_export_fp8_block2d(const void *x, uint8_t *y, int64_t rows, int64_t cols
     constexpr int N = Vec<T>::N;
     if (cols % N != 0 || block_cols % N != 0 || !aligned16(x) || ((uintptr_t)y % N) != 0)
       return MTQ_ERR_INVALID_ARG;
-    const int64_t nvec = rows * cols / N, cv = cols / N;
+    const int64_t nvec = rows * cols / N, cv = cols / N, bcv = block_cols / N;
     const int64_t ncb = (cols + block_cols - 1) / block_cols;
-    export_fp8_blk2d_kernel<T><<<(unsigned)((nvec + kThreads - 1) / kThreads), kThreads, 0, stream>>>(
-        reinterpret_cast<const T *>(x), y, nvec, cv, block_rows, block_cols / N, ncb, scale, round_to_dtype, 1);
+    const bool i32 = nvec < (1ll << 31) && block_rows < (1ll << 31);
+    const FastDiv fcv = make_fastdiv(i32 ? (uint32_t)cv : 1u), fbr = make_fastdiv(i32 ? (uint32_t)block_rows : 1u),
+                  fbcv = make_fastdiv(i32 ? (uint32_t)bcv : 1u);
+    constexpr int U = 2;
+    if (i32)
+      export_fp8_blk2d_kernel<U, T, true><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, nvec, cv, fcv, block_rows, fbr, bcv, fbcv, ncb, scale, round_to_dtype, 1);
+    else
+      export_fp8_blk2d_kernel<U, T, false><<<export_grid(nvec, U), kThreads, 0, stream>>>(
+          reinterpret_cast<const T *>(x), y, nvec, cv, fcv, block_rows, fbr, bcv, fbcv, ncb, scale, round_to_dtype, 1);
     return check_launch();
   });
 }

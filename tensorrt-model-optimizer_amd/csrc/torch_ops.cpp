@@ -961,17 +961,17 @@ at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hma
     bp = b.data_ptr<int64_t>();
   }
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  // all-zero [chunks * bins + 1] int32, left all zero by the launch: the caller's reusable one, or
-  // a fresh one
+  // the per-workgroup count rows (any contents, overwritten): the caller's buffer when it is large
+  // enough, else a fresh one from the caching allocator
+  const int64_t words = mtq_histogram_chunked_scratch_words(x.numel(), (int)chunks, (int)bins);
+  TORCH_CHECK(words >= 0, "histogram_abs_chunked: bad size");
   at::Tensor scratch;
   if (scratch_in.has_value() && scratch_in->defined()) {
     scratch = *scratch_in;
-    TORCH_CHECK(scratch.scalar_type() == at::kInt && scratch.is_contiguous() && scratch.device() == x.device() &&
-                    scratch.numel() >= chunks * bins,
-                "histogram_abs_chunked: scratch must be contiguous int32 [>= chunks * bins] on the input's device");
-  } else {
-    scratch = at::zeros({chunks * bins}, x.options().dtype(at::kInt));
+    TORCH_CHECK(scratch.scalar_type() == at::kInt && scratch.is_contiguous() && scratch.device() == x.device(),
+                "histogram_abs_chunked: scratch must be contiguous int32 on the input's device");
   }
+  if (!scratch.defined() || scratch.numel() < words) scratch = at::empty({words > 0 ? words : 1}, x.options().dtype(at::kInt));
   // accum: a running fp32 histogram added into the result (its first accum.numel() bins)
   at::Tensor accum;
   if (accum_in.has_value() && accum_in->defined()) {
@@ -984,7 +984,7 @@ at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hma
   int st = mtq_histogram_abs_chunked(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"),
                                      hmax.data_ptr<float>(), (int)bins, skip_zeros ? 1 : 0, bp,
                                      chunk_elems, (int)chunks,
-                                     reinterpret_cast<uint32_t *>(scratch.data_ptr<int32_t>()),
+                                     reinterpret_cast<uint32_t *>(scratch.data_ptr<int32_t>()), scratch.numel(),
                                      accum.defined() ? accum.data_ptr<float>() : nullptr,
                                      accum.defined() ? accum.numel() : 0, hist.data_ptr<float>(),
                                      cur_stream(x));

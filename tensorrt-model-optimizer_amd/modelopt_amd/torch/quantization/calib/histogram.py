@@ -143,19 +143,6 @@ _HISTC_GRAIN = 32768  # at::internal::GRAIN_SIZE: the parallel_for grain of the 
 _F32_COUNT_LIMIT = 2**24  # an fp32 counter stops here: 2^24 + 1 rounds to 2^24 (ties to even)
 
 
-# All-zero int32 scratch of the one-launch chunked histogram (the launch leaves it zero again),
-# one per (device, stream): calls on one stream are ordered, so they can share it.
-_CHUNK_SCRATCH: dict = {}
-
-
-def _chunk_scratch(device: torch.device, words: int) -> torch.Tensor:
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
-    buf = _CHUNK_SCRATCH.get(key)
-    if buf is None or buf.numel() < words:
-        buf = _CHUNK_SCRATCH[key] = torch.zeros(max(words, 16 * 8192), dtype=torch.int32, device=device)
-    return buf
-
-
 def _histc_threads() -> int:
     env = os.environ.get("MTQ_AMD_HIST_THREADS")
     return max(1, int(env)) if env else max(1, torch.get_num_threads())
@@ -195,12 +182,7 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
         # block per boundary), no host sync; with at most 2^24 non-zeros every count is exact in
         # fp32, so the chunked sum equals the single-launch count there too
         t = threads or _histc_threads()
-        scratch = _chunk_scratch(flat.device, t * bins)
-        try:
-            return ops.histogram_abs_chunked_nonzero(flat, hmax, bins, t, scratch, accum)
-        except Exception:
-            _CHUNK_SCRATCH.clear()
-            raise
+        return ops.histogram_abs_chunked_nonzero(flat, hmax, bins, t, None, accum)
     if skip_zeros:
         # chunk boundaries live in the compacted (non-zero) index space: map them back
         csum = torch.cumsum((flat != 0).to(torch.int64), 0)
@@ -219,14 +201,10 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
         # the first original index whose non-zero rank reaches each compacted start
         cuts = torch.searchsorted(csum, torch.tensor(starts[1:-1], device=csum.device, dtype=torch.int64) + 1)
     if gpu_one_launch:
-        # one launch counts every chunk into its own row; its last workgroup adds the clamped rows in order
+        # one launch counts every chunk (per-workgroup rows), a second adds the clamped chunk
+        # counts in order (scratch: the caching allocator's, any contents)
         nch = len(starts) - 1
-        scratch = _chunk_scratch(flat.device, nch * bins)
-        try:
-            return ops.histogram_abs_chunked(flat, hmax, bins, False, None, chunk, nch, scratch, accum)
-        except Exception:
-            _CHUNK_SCRATCH.clear()  # a failed launch may leave it non-zero
-            raise
+        return ops.histogram_abs_chunked(flat, hmax, bins, False, None, chunk, nch, None, accum)
     bounds = [0] + cuts.tolist() + [n] if cuts is not None else starts
     hist = torch.zeros(bins, dtype=torch.float32, device=x.device)
     counts = torch.empty(bins, dtype=torch.int32, device=x.device)

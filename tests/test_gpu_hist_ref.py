@@ -167,10 +167,11 @@ def test_histc_chunked_single_launch_matches_per_chunk_counts(gpu, dtype):
     assert float(got.max()) == float(F32) and float(got.sum()) == float(F32)
 
 
-def test_histc_chunked_scratch_left_zero_and_reusable(gpu):
-    """The one-launch chunked histogram leaves its scratch (rows + block counter) all zero, so one
-    buffer serves every call on a stream: back-to-back calls with varying chunk counts / bins on
-    one scratch give the results of fresh-scratch calls."""
+def test_histc_chunked_scratch_any_contents_and_reusable(gpu):
+    """The chunked histogram overwrites every per-workgroup row of its scratch, so a caller's
+    buffer holding garbage, reused across calls with varying chunk counts / bins, gives the
+    results of fresh-scratch calls; a buffer below mtq_histogram_chunked_scratch_words is
+    replaced by a fresh one, not overrun."""
     from modelopt_amd import _ext
 
     ops = _ext.ops()
@@ -178,14 +179,16 @@ def test_histc_chunked_scratch_left_zero_and_reusable(gpu):
     n = 8 * 1_500_001
     x = (torch.randn(n, device=gpu, generator=g) * 3).to(torch.bfloat16)
     hmax = torch.tensor([8.0], device=gpu)
-    scratch = torch.zeros(16 * 4096 + 1, dtype=torch.int32, device=gpu)
+    scratch = torch.randint(-2**31, 2**31 - 1, (1 << 22,), dtype=torch.int32, device=gpu, generator=g)
+    small = torch.full((64,), 7, dtype=torch.int32, device=gpu)
     for chunks, bins in ((16, 2048), (3, 4096), (7, 1000), (16, 2048)):
         chunk = -(-n // chunks)
         fresh = ops.histogram_abs_chunked(x, hmax, bins, False, None, chunk, chunks)
         for _ in range(2):
             got = ops.histogram_abs_chunked(x, hmax, bins, False, None, chunk, chunks, scratch)
             assert torch.equal(got, fresh), (chunks, bins)
-            assert int(scratch.abs().sum()) == 0, "scratch not left zero"
+        assert torch.equal(ops.histogram_abs_chunked(x, hmax, bins, False, None, chunk, chunks, small), fresh)
+        assert int((small != 7).sum()) == 0, "a too-small scratch was written"
 
 
 def _host_nonzero_bounds(x, threads, grain=32768):
