@@ -16,7 +16,7 @@ import torch  # noqa: E402
 from modelopt_amd import _ext  # noqa: E402
 
 ops = _ext.ops()
-lib = ctypes.CDLL(str(REPO / "scripts/exp/libexport_exp.so"))
+lib = ctypes.CDLL(str(Path(__file__).resolve().parent / "libexport_exp.so"))
 lib.export_exp.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
 VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "5,6,7,8,9,10".split(","))]
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 7
@@ -45,6 +45,8 @@ def var(v):
 
 
 for v in VARS:
+    if v == 15:  # probe: output deliberately wrong
+        continue
     for x in xs[:2]:
         yp, sp = product(x)
         ys.fill_(0x5A)

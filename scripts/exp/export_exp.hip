@@ -42,7 +42,10 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_pf_kernel(const T *__re
 // workgroup's 128 scale bytes gathered in LDS and written by 32 lanes as one 128 B line instead of
 // 8 waves x 2 x 16 B non-temporal fragments.  bf16, block 32, native path (a lane whose block
 // leaves it falls back to the product function).
-template <bool SNT, bool DNT, bool LDS, int U = 2>
+// MODE 1: the scale exponent branch-free for normal amax / 6 outside 0 < mantissa <= 64 (ex + (m != 0)),
+// the product function only for the rare rest; MODE 2: probe -- no conversion (codes = amax bits),
+// the structure's memory floor (output wrong)
+template <bool SNT, bool DNT, bool LDS, int U = 2, int MODE = 0>
 __global__ __launch_bounds__(kThreads) void export_mxfp4_st_kernel(const __bf16 *__restrict__ x, uint8_t *__restrict__ y,
                                                                    uint8_t *__restrict__ sc, int64_t nvec) {
   using T = __bf16;
@@ -70,7 +73,21 @@ __global__ __launch_bounds__(kThreads) void export_mxfp4_st_kernel(const __bf16 
     const float amax = half_bits_to_float<T>(m);
     constexpr float kInv6 = 1.0f / 6.0f;
     const float d6 = amax <= 3.402823466e38f ? div_rn(amax, 6.0f, kInv6) : amax * kInv6;
-    const float e = mx_e8m0_exponent(d6);
+    float e;
+    if constexpr (MODE == 1) {
+      const uint32_t db = __float_as_uint(d6), ef = (db >> 23) & 0xFFu, mm = db & 0x7FFFFFu;
+      e = (float)((int)ef - 127 + (mm != 0u ? 1 : 0));
+      if (db == 0u) e = -127.f;
+      else if (!((ef - 1u) < 0xFEu && (mm == 0u || mm > 64u))) e = mx_e8m0_exponent(d6);
+    } else if constexpr (MODE == 2) {
+      e = 0.f;
+      uint32_t *dy = reinterpret_cast<uint32_t *>(y + i * 4);
+      __builtin_nontemporal_store(m, dy);
+      if (threadIdx.x % LPB == 0) sl[u * (kThreads / LPB) + threadIdx.x / LPB] = (uint8_t)m;
+      continue;
+    } else {
+      e = mx_e8m0_exponent(d6);
+    }
     if (!(e >= -100.f && e <= 127.f)) {  // exact path, product function (writes its own scale)
       export_mxfp4_vec_one<T, 32, true>(i, v[u], y, sc, nvec, 0);
       if constexpr (LDS) {
@@ -145,6 +162,9 @@ extern "C" int export_exp(int var, const void *x, uint8_t *y, uint8_t *scales, i
   case 11: export_mxfp4_st_kernel<true, true, true, 4><<<export_grid(nvec, 4), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   case 12: export_mxfp4_st_kernel<true, true, true, 8><<<export_grid(nvec, 8), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   case 13: export_mxfp4_st_kernel<true, true, true, 1><<<export_grid(nvec, 1), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 14: export_mxfp4_st_kernel<true, true, true, 4, 1><<<export_grid(nvec, 4), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 15: export_mxfp4_st_kernel<true, true, true, 4, 2><<<export_grid(nvec, 4), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
+  case 16: export_mxfp4_st_kernel<true, true, true, 2, 1><<<export_grid(nvec, 2), kThreads, 0, stream>>>(xt, y, scales, nvec); break;
   default: return 3;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -415,19 +415,42 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // max over aligned groups of G consecutive lanes (G power of two <= 64)
+// Cross-lane moves inside a row of 16 lanes on the DPP path of the VALU (no LDS round trip, no
+// lgkmcnt wait): xor 1 / xor 2 as quad permutations, then the half-row and row mirrors (lane i
+// <- 7 - i / 15 - i), which pair every lane with one of the other half once the smaller groups are
+// reduced -- enough for a max.  Groups of 32 / 64 keep __shfl_xor (ds_bpermute).
+template <int CTRL> __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
 template <int G> __device__ __forceinline__ uint32_t group_max_u32(uint32_t v) {
+  if constexpr (G <= 16) {
+    if constexpr (G >= 2) v = max(v, dpp_u32<0xB1>(v));   // quad_perm [1, 0, 3, 2]
+    if constexpr (G >= 4) v = max(v, dpp_u32<0x4E>(v));   // quad_perm [2, 3, 0, 1]
+    if constexpr (G >= 8) v = max(v, dpp_u32<0x141>(v));  // row_half_mirror
+    if constexpr (G >= 16) v = max(v, dpp_u32<0x140>(v)); // row_mirror
+    return v;
+  } else {
 #pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) {
-    uint32_t t = (uint32_t)__shfl_xor((int)v, o, 64);
-    v = t > v ? t : v;
+    for (int o = G / 2; o > 0; o >>= 1) {
+      uint32_t t = (uint32_t)__shfl_xor((int)v, o, 64);
+      v = t > v ? t : v;
+    }
+    return v;
   }
-  return v;
 }
 
 template <int G> __device__ __forceinline__ float group_max_f(float v) {
+  if constexpr (G <= 16) {
+    if constexpr (G >= 2) v = fmaxf(v, __uint_as_float(dpp_u32<0xB1>(__float_as_uint(v))));
+    if constexpr (G >= 4) v = fmaxf(v, __uint_as_float(dpp_u32<0x4E>(__float_as_uint(v))));
+    if constexpr (G >= 8) v = fmaxf(v, __uint_as_float(dpp_u32<0x141>(__float_as_uint(v))));
+    if constexpr (G >= 16) v = fmaxf(v, __uint_as_float(dpp_u32<0x140>(__float_as_uint(v))));
+    return v;
+  } else {
 #pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+    for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+  }
 }
 
 // ---- fast unsigned division by a run-time constant (Granlund-Montgomery), n < 2^31 ----------

@@ -2212,22 +2212,15 @@ __global__ __launch_bounds__(kThreads) void export_nvfp4_kernel(const T *__restr
 // the exponent bits unless the significand is within 2^-10 of a power of two, where the rounding
 // of log2 can land on the integer -- only then is a double log2 taken.
 __device__ __forceinline__ float mx_e8m0_exponent(float d) {
+  const uint32_t b = __float_as_uint(d);
+  const uint32_t m = b & 0x7fffffu;
+  // positive normal d with m == 0 (log2 exact) or m > 64 (log2(d) = ex + log2(1 + m 2^-23) rounds
+  // above ex for every such m; the largest m that rounds back to ex is 22: scripts/check_e8m0.c,
+  // exhaustive): ceil = ex + (m != 0), one test and no nested branches -- all but 1 block in 2^17
+  if ((b >> 23) - 1u < 0xFEu && (m == 0u || m > 64u)) return (float)((int)(b >> 23) - 127 + (m != 0u ? 1 : 0));
   if (d != d) return d;
   if (!(d > 0.f)) return -127.f;
-  const uint32_t b = __float_as_uint(d);
-  const int ex = (int)((b >> 23) & 0xff) - 127;
-  const uint32_t m = b & 0x7fffffu;
-  float e;
-  if (((b >> 23) & 0xff) != 0 && m == 0) {
-    e = (float)ex;
-  } else if (((b >> 23) & 0xff) != 0 && m > 64u) {
-    // log2(d) = ex + log2(1 + m 2^-23) rounds above ex for every normal d with m > 64 (the largest
-    // m that rounds back to ex is 22: scripts/check_e8m0.c, exhaustive), so ceil gives ex + 1 --
-    // the double-precision log2 below runs for 1 block in 2^17 instead of 1 in 2^10
-    e = (float)(ex + 1);
-  } else {
-    e = __builtin_ceilf((float)log2((double)d));
-  }
+  const float e = __builtin_ceilf((float)log2((double)d));  // subnormal d, or 0 < m <= 64
   return e > -127.f ? e : -127.f;
 }
 
