@@ -2912,8 +2912,7 @@ __global__ __launch_bounds__(kThreads) void export_mxfp8_kernel(const T *__restr
     const uint32_t b = __float_as_uint(f[j]) & 0x7fffffffu;
     m = b > m ? b : m;
   }
-  m = max(m, (uint32_t)__shfl_xor((int)m, 1));
-  m = max(m, (uint32_t)__shfl_xor((int)m, 2));
+  m = group_max_u32<4>(m);
   const float amax = __uint_as_float(m > 0x7f800000u ? 0x7fc00000u : m);
   const float descale = amax / 448.0f;
   float e = descale > 0.f ? mx_e8m0_exponent(descale) : -127.f;
