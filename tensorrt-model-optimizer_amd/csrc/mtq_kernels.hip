@@ -2427,23 +2427,37 @@ __device__ __forceinline__ uint32_t int4_pair_nan(float d, float x) {
   return (uint32_t)v & 0xFu;
 }
 
-// rows (2p, 2p+1) x N columns -> N bytes
+// rows (2p, 2p+1) x N columns -> N bytes, in two phases so a thread's U vector pairs are all
+// loaded before the first is packed (r05: with load and pack in one function per vector, the
+// second pair's loads were issued only after the first pair's store)
+template <typename T>
+struct Int4Pair {
+  Vec<T> lo, hi;
+  float s0, s1;
+  int64_t out;  // byte offset of the N packed bytes
+};
 template <typename T, bool IDX32>
-__device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restrict__ x,
-                                                                    uint8_t *__restrict__ y,
-                                                                    int64_t nvec, int64_t cols,
-                                                                    FastDiv fcv, FastDiv fblk,
-                                                                    const float *__restrict__ scale,
-                                                                    int64_t nblk, int block) {
-  using V = Vec<T>;
-  constexpr int N = V::N;
-  if (i >= nvec) return;
+__device__ __forceinline__ Int4Pair<T> export_int4_load(int64_t i, const T *__restrict__ x, int64_t cols,
+                                                        FastDiv fcv, FastDiv fblk, const float *__restrict__ scale,
+                                                        int64_t nblk, int block) {
+  constexpr int N = Vec<T>::N;
   const int64_t cv = cols / N;
   const int64_t pr = idx_div<IDX32>(i, cv, fcv), c0 = (i - pr * cv) * N;
-  V lo = ldg_vec_nt(x + (2 * pr) * cols + c0);
-  V hi = ldg_vec_nt(x + (2 * pr + 1) * cols + c0);
+  Int4Pair<T> q;
+  q.lo = ldg_vec_nt(x + (2 * pr) * cols + c0);
+  q.hi = ldg_vec_nt(x + (2 * pr + 1) * cols + c0);
   const int64_t cb = idx_div<IDX32>(c0, block, fblk);
-  const float s0 = scale[(2 * pr) * nblk + cb], s1 = scale[(2 * pr + 1) * nblk + cb];
+  q.s0 = scale[(2 * pr) * nblk + cb];
+  q.s1 = scale[(2 * pr + 1) * nblk + cb];
+  q.out = pr * cols + c0;
+  return q;
+}
+template <typename T>
+__device__ __forceinline__ void export_int4_pack(const Int4Pair<T> &q, uint8_t *__restrict__ y) {
+  using V = Vec<T>;
+  constexpr int N = V::N;
+  const V &lo = q.lo, &hi = q.hi;
+  const float s0 = q.s0, s1 = q.s1;
   const float r0 = 1.0f / s0, r1 = 1.0f / s1;
   // div_rn is the IEEE quotient except where that quotient overflows or is infinite (div_rn
   // gives NaN there, IEEE +-inf -> the clamp's -8 / 7, selected from the weight's sign) and where
@@ -2489,10 +2503,10 @@ __device__ __forceinline__ void export_int4_vec_one(int64_t i, const T *__restri
       b[j] = int4_pair(Elem<T>::ld(lo.e[j]) / s0, Elem<T>::ld(hi.e[j]) / s1);
   }
   if constexpr (N == 8)
-    st_packed_nt(y + pr * cols + c0, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
+    st_packed_nt(y + q.out, b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
                  b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
   else
-    st_packed_nt(y + pr * cols + c0, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
+    st_packed_nt(y + q.out, (uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)));
 }
 
 // one 16 B vector (N elements of one block) -> N/2 bytes
@@ -2831,9 +2845,15 @@ __global__ __launch_bounds__(kThreads) void export_int4_vec_kernel(const T *__re
                                                                     const float *__restrict__ scale,
                                                                     int64_t nblk, int block) {
   const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  Int4Pair<T> q[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // unconditional (clamped) loads: see export_mxfp4_vec_kernel
+    const int64_t i = base + u * kThreads;
+    q[u] = export_int4_load<T, IDX32>(i < nvec ? i : nvec - 1, x, cols, fcv, fblk, scale, nblk, block);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    export_int4_vec_one<T, IDX32>(base + u * kThreads, x, y, nvec, cols, fcv, fblk, scale, nblk, block);
+    if (base + u * kThreads < nvec) export_int4_pack<T>(q[u], y);
 }
 template <int U, typename T, bool IDX32>
 __global__ __launch_bounds__(kThreads) void export_nvfp4_vec_kernel(const T *__restrict__ x,
