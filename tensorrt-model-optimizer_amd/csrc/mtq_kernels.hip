@@ -1475,11 +1475,12 @@ int64_t hist_chunk_bpc(int64_t n, int chunks) {
 // group in chunk order (torch.histc's thread-order fold of its fp32 per-thread counts), group
 // after group, then + accum[b] for b < accum_n (the calibrator's running histogram,
 // `hist[:old.numel()] += old`).
-__global__ __launch_bounds__(1024) void hist_fold_blocks_kernel(const uint32_t *__restrict__ rows, int bpc,
-                                                                int chunks, int bins, const float *accum,
-                                                                int64_t accum_n, float *hist) {  // accum may alias hist
-  __shared__ float part[16][64];
-  const int bl = threadIdx.x & 63, cl = threadIdx.x >> 6, b = blockIdx.x * 64 + bl;
+template <int BW>  // bins per workgroup; BW * 16 threads
+__global__ __launch_bounds__(BW * 16) void hist_fold_blocks_kernel(const uint32_t *__restrict__ rows, int bpc,
+                                                                   int chunks, int bins, const float *accum,
+                                                                   int64_t accum_n, float *hist) {  // accum may alias hist
+  __shared__ float part[16][BW];
+  const int bl = threadIdx.x % BW, cl = threadIdx.x / BW, b = blockIdx.x * BW + bl;
   float h = 0.f;
   for (int c0 = 0; c0 < chunks; c0 += 16) {
     const int c = c0 + cl;
@@ -3305,7 +3306,10 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
       count_dispatch(kDispHistValueChunked);
       kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
                                                                       hmax, bins, skip_zeros, nullptr, ch);
-      hist_fold_blocks_kernel<<<(unsigned)((bins + 63) / 64), 1024, 0, stream>>>(scratch, (int)bpc, chunks, bins,
+      // 64 bins x 16 chunks per 1024-thread workgroup (16 x 16 per 256 threads: 4.99 vs 4.75-4.90 us
+      // in the kernel trace, r05)
+      constexpr int kFoldBW = 64;
+      hist_fold_blocks_kernel<kFoldBW><<<(unsigned)((bins + kFoldBW - 1) / kFoldBW), kFoldBW * 16, 0, stream>>>(scratch, (int)bpc, chunks, bins,
                                                                                  accum, accum_n, hist);
       return check_launch();
     }
