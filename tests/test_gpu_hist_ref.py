@@ -129,7 +129,8 @@ def test_histc_exact_counts_mode(gpu, monkeypatch):
 def test_histc_chunked_single_launch_matches_per_chunk_counts(gpu, dtype):
     """histogram_abs_chunked (every chunk in one launch, rows summed in chunk order) against the
     per-chunk launches over slices: chunk edges off the 8-element vectors, uniform and explicit
-    (skip_zeros-style) bounds, 1..16 chunks, a bin past 2^24 in the sum."""
+    (skip_zeros-style) bounds, 1..300 chunks (more than 16: the fold adds its chunk groups in
+    order; more than the CUs: one workgroup per chunk), a bin past 2^24 in the sum."""
     from modelopt_amd import _ext
 
     ops = _ext.ops()
@@ -150,7 +151,7 @@ def test_histc_chunked_single_launch_matches_per_chunk_counts(gpu, dtype):
             h += c.float().clamp_(max=F32)
         return h
 
-    for chunks in (1, 3, 16):
+    for chunks in (1, 3, 16, 17, 40, 300):
         chunk = -(-n // chunks)
         bounds = [min(t * chunk, n) for t in range(chunks)] + [n]
         for skip in (False, True):
