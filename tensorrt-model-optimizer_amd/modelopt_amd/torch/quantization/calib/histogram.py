@@ -156,11 +156,12 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     so one launch does.  Above that, the chunk of thread t of at::parallel_for (``T = threads``,
     default ``_histc_threads()``; chunk = ceil(N / T), N = elements after ``skip_zeros``) is counted
     exactly, clamped at 2^24 and added into the fp32 result in thread order: bf16 / f16 on the GPU
-    in one launch for all chunks (histogram_abs_chunked; with ``skip_zeros`` the non-zero chunk
-    boundaries are found on the device first, histogram_abs_chunked_nonzero), other inputs one
-    launch per chunk.  ``accum`` (the calibrator's running histogram, ``numel <= bins``) is added
-    into the first bins of the result (``hist[:old.numel()] += old``, reference histogram.py:127),
-    in the chunk fold's launch on the one-launch path."""
+    in one counting launch for all chunks plus one fold launch (histogram_abs_chunked; with
+    ``skip_zeros`` the non-zero chunk boundaries are found on the device first,
+    histogram_abs_chunked_nonzero), other inputs one launch per chunk.  ``accum`` (the
+    calibrator's running histogram, ``numel <= bins``) is added into the first bins of the result
+    (``hist[:old.numel()] += old``, reference histogram.py:127), in the fold launch on the GPU
+    path."""
 
     def plus_accum(hist):
         if accum is not None:
