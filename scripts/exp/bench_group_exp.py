@@ -43,11 +43,11 @@ def prod(i):
 
 
 ref = prod(0).view(-1)
-for v in (0, 1):
+for v in (0, 1, 2, 3, 4):
     var(v)(0)
     torch.cuda.synchronize()
     assert torch.equal(y.view(-1), ref), v
-arms = {"v0_product": var(0), "v1_clamped": var(1)}
+arms = {"v0_product": var(0), "v1_clamped": var(1), "v2_tpb512": var(2), "v3_tpb1024": var(3), "v4_tpb256": var(4), "product_op": lambda i: prod(i)}
 t = {k: [] for k in arms}
 for _ in range(ROUNDS):
     for k, f in arms.items():

@@ -351,16 +351,19 @@ __global__ __launch_bounds__(kThreads) void ew_group_kernel(const T *__restrict_
 // scalar loads from one wave-uniform address (scalar cache, no vector-memory instruction, no
 // per-lane address) and each lane selects its own.  FP8 block-128 bf16 [32768, 4096]: 88.3 ->
 // 83.4-84.9 us (76.6 -> 79.7-81.1 % of HBM peak, profiles/r02/export/).
+// TPB = 512 threads per workgroup: 0.5-0.8 % faster than 256 on the bench primary in interleaved
+// A/Bs (83.1 vs 83.6 us; 1024: 86.2 us; scripts/exp/group_exp.hip, profiles/r05/group_tpb_ab_r05gx3.log)
+constexpr int kGroupSkThreads = 512;
 template <typename T, class Op, int U, int LPB>
-__global__ __launch_bounds__(kThreads) void ew_group_sk_kernel(const T *__restrict__ x,
-                                                                T *__restrict__ y, int64_t nvec,
-                                                                const float *__restrict__ amax,
-                                                                int64_t nchan, Op op) {
+__global__ __launch_bounds__(kGroupSkThreads) void ew_group_sk_kernel(const T *__restrict__ x,
+                                                                       T *__restrict__ y, int64_t nvec,
+                                                                       const float *__restrict__ amax,
+                                                                       int64_t nchan, Op op) {
   using V = Vec<T>;
   constexpr int CPW = 64 / LPB;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t wb = ((int64_t)blockIdx.x * kThreads + (int64_t)w * 64) * U;
+  const int64_t wb = ((int64_t)blockIdx.x * kGroupSkThreads + (int64_t)w * 64) * U;
   const int k = lane / LPB, pos = lane - k * LPB;
   const int64_t v0 = wb + (int64_t)k * LPB * U + pos;
   V v[U];
@@ -473,7 +476,9 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
         auto go = [&](auto lc) {
           constexpr int L = decltype(lc)::value;
           count_dispatch(kDispEwGroupSk);
-          ew_group_sk_kernel<T, VecOp<T>, U, L><<<g, kThreads, 0, stream>>>(
+          const unsigned gsk =
+              (unsigned)((nvec + (int64_t)kGroupSkThreads * U - 1) / ((int64_t)kGroupSkThreads * U));
+          ew_group_sk_kernel<T, VecOp<T>, U, L><<<gsk, kGroupSkThreads, 0, stream>>>(
               reinterpret_cast<const T *>(x), reinterpret_cast<T *>(y), nvec,
               reinterpret_cast<const float *>(op.amax), axis_size, op);
         };
