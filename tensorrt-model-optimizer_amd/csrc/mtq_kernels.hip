@@ -1988,24 +1988,24 @@ __global__ __launch_bounds__(kThreads) void nvfp4_vec_kernel(const T *__restrict
 // U = 2 vectors per lane, both loads issued before the first block is converted, the per-thread
 // constants (global scale, its 6x reciprocal) paid once per U vectors: 0.755-0.760 -> 0.772-0.774
 // of the HBM roofline over one vector per lane, U = 4 slower (profiles/r03/nvfp4).
-template <typename T, int BS, int U>
-__global__ __launch_bounds__(kThreads) void nvfp4_native_u_kernel(const T *__restrict__ x,
-                                                                   T *__restrict__ y, int64_t nvec,
-                                                                   const float *__restrict__ gamax) {
+template <typename T, int BS, int U, int TPB = kThreads>
+__global__ __launch_bounds__(TPB) void nvfp4_native_u_kernel(const T *__restrict__ x,
+                                                              T *__restrict__ y, int64_t nvec,
+                                                              const float *__restrict__ gamax) {
   using V = Vec<T>;
   constexpr int N = V::N;
   static_assert(N == 8 && BS % N == 0, "16-bit elements, block a multiple of the vector");
   constexpr int LPB = BS / N;
-  const int64_t base = (int64_t)blockIdx.x * (kThreads * U) + threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (TPB * U) + threadIdx.x;
   const int lead = threadIdx.x % LPB;  // a block's LPB lanes are in range together
   V v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    if (base + u * kThreads - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * kThreads) * N);
+    if (base + u * TPB - lead < nvec) v[u] = ldg_vec_nt(x + (base + u * TPB) * N);
   const float gs = nvfp4_global_scale(gamax);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int64_t i = base + u * kThreads;
+    const int64_t i = base + u * TPB;
     if (i - lead >= nvec) continue;
     uint32_t w[4] = {v[u].raw.x, v[u].raw.y, v[u].raw.z, v[u].raw.w};
     const PairScan sc = scan_pairs(w);
