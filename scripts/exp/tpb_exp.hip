@@ -1,6 +1,8 @@
 // tpb_exp.hip -- measurement-only A/B of workgroup size on the dynamic NVFP4 qdq kernel
 // (csrc/mtq_kernels.hip nvfp4_native_u_kernel, block 16, U = 2): var = threads per workgroup
 // (256 = the product launch, 512, 1024).  Built by build_exp.sh, timed by bench_tpb_exp.py.
+// r05 (profiles/r05/nvfp4_tpb_ab_r05tp1.log): 512 within 0.2-0.5 % of 256, 1024 6 % slower -- the
+// launch stays at 256 (unlike the bench primary's group kernel, where 512 gained ~1 %).
 #include "../../tensorrt-model-optimizer_amd/csrc/mtq_kernels.hip"
 
 extern "C" int tpb_exp(int var, const void *x, void *y, int64_t n, const float *gamax, hipStream_t stream) {
