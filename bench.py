@@ -20,6 +20,9 @@ Also reported (same JSON line):
                 slowest rank), the bf16 forward of the same batches at N=1, and the difference
   ptq_c3        Llama-3-8B INT4 AWQ-lite (block 128) PTQ wall-clock, same calibration set
   ptq_c5        Mixtral-8x7B FP8 PTQ wall-clock beside its bf16 forward (N=1 by default)
+  ptq_c4        Llama-3-70B MXFP4 W+A PTQ wall-clock beside its bf16 forward: the whole model on one
+                GPU at N=1, the decoder layers sharded over the ranks at N>1 (RCCL point-to-point
+                hand-off between stages + one packed all_reduce(MAX) of the amax state)
 
 Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one rank per GPU: under
 torch.distributed.run when RANK is set, otherwise bench.py starts that launcher itself as a child
@@ -429,6 +432,10 @@ def main():
                     help="skip C5: Mixtral-8x7B FP8 PTQ (93 GB bf16 resident, ~40 s) beside its bf16 forward; it runs "
                     "by default at N=1")
     ap.add_argument("--c5", action="store_true", help="run C5 at N > 1 too (data-parallel, 93 GB per rank)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip C4: Llama-3-70B MXFP4 W+A PTQ (141 GB bf16 at N=1; layer-sharded over the ranks at N>1)")
+    ap.add_argument("--c4-dims", choices=("llama3-70b", "tiny"), default=None,
+                    help="C4 model dims (default: llama3-70b on the GPU, tiny for the --device cpu rehearsal)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
                     help="cpu = plumbing rehearsal on the product's host kernels (default: cuda when a "
@@ -439,7 +446,10 @@ def main():
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(_self_launch(args.gpus))
     device = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    if device == "cpu":  # the GPU-only legs need a device
+    # the GPU-only legs need a device; the C4 leg's plumbing (layer-sharded pipeline, packed
+    # amax exchange) also runs on the host at tiny dims
+    run_c4 = not (args.no_ptq or args.no_c4)
+    if device == "cpu":
         args.no_suite = args.no_ptq = True
     dist, rank, world = _dist_init(args.gpus, device)
     from modelopt_amd import _ext
@@ -540,6 +550,20 @@ def main():
             if "bf16_forward_s" in r5:
                 r5["overhead_frac"] = round(r5["ptq_wall_clock_s"] / r5["bf16_forward_s"] - 1.0, 4)
             out["ptq_c5"] = r5
+    if run_c4:
+        # C4: Llama-3-70B MXFP4 W+A (block 32, E8M0) PTQ; whole model at N=1, layer-sharded at N>1
+        from benchmarks import ptq_c4  # noqa: PLC0415
+
+        dims = args.c4_dims or ("tiny" if device == "cpu" else "llama3-70b")
+        print(f"bench: C4 {dims} MXFP4_DEFAULT_CFG PTQ ...", file=sys.stderr, flush=True)
+        if device == "cuda":
+            torch.cuda.empty_cache()
+        _barrier(dist)
+        small = dict(samples=16, seq=64, batch=4) if dims == "tiny" else dict(samples=512, seq=512, batch=16)
+        with contextlib.redirect_stdout(sys.stderr):
+            out["ptq_c4"] = ptq_c4.run(**small, dims=dims, baseline=True,
+                                       device=torch.device("cuda", torch.cuda.current_device()) if device == "cuda"
+                                       else torch.device("cpu"))
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_ptq:

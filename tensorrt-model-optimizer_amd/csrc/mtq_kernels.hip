@@ -425,7 +425,8 @@ __global__ __launch_bounds__(kThreads) void ew_rowwave_kernel(const T *__restric
     // 16-bit scalar load, and the vector load the compiler emits otherwise put a VMEM round trip
     // in front of every wave's first store: 0.746 vs 0.777 with an fp32 amax, r05n).  amax is
     // 4-byte aligned (the launcher checks), so the dword of an even-count tensor's last element
-    // is inside it and an odd count's last dword ends 2 bytes past it, inside the allocation.
+    // is inside it (the launcher takes this path for an even channel count only, so no dword
+    // reaches past the tensor).
     const uint32_t wv = reinterpret_cast<const uint32_t *>(amax)[c >> 1];
     const uint16_t h = (uint16_t)((c & 1) ? (wv >> 16) : (wv & 0xFFFFu));
     am = Elem<A>::ld(__builtin_bit_cast(A, h));
@@ -502,10 +503,12 @@ int launch_axis(const void *x, void *y, int64_t n, int64_t axis_size, int64_t in
       return check_launch();
     }
     // long channels (per-row weights): channel length a multiple of 128 vectors, fp32 amax,
-    // 16-byte aligned, no outer wrap -> wave-uniform channel
+    // 16-byte aligned, no outer wrap -> wave-uniform channel.  A 16-bit amax is read as the
+    // dword holding it, so that form needs a 4-byte-aligned amax and an even channel count (the
+    // last dword then ends at the tensor's end); odd counts take the element-wise kernel
     const bool amax_own = ((op.amax_dtype == MTQ_BF16 && __is_same(T, __bf16)) ||
                            (op.amax_dtype == MTQ_F16 && __is_same(T, _Float16))) &&
-                          reinterpret_cast<uintptr_t>(op.amax) % 4 == 0;
+                          reinterpret_cast<uintptr_t>(op.amax) % 4 == 0 && axis_size % 2 == 0;
     if (vb >= 128 && vb % 128 == 0 && aligned16(x) && aligned16(y) &&
         (op.amax_dtype == MTQ_F32 || amax_own) && axis_size * vb == n / N && n % N == 0) {
       constexpr int U = 2;

@@ -396,8 +396,19 @@ def _mse_fast(out, ref) -> bool:
 _AWQ_FUSED_MAX_N = 2048
 _AWQ_FUSED_MAX_G = 64
 _AWQ_FUSED = os.environ.get("MTQ_AMD_AWQ_FUSED", "auto")
-if _AWQ_FUSED not in ("auto", "always", "library", "never"):
-    raise ValueError(f"MTQ_AMD_AWQ_FUSED={_AWQ_FUSED!r}: expected auto, always, library or never")
+_AWQ_FUSED_CHOICES = ("auto", "always", "library", "never")
+
+
+def _check_awq_fused() -> None:
+    """Validate MTQ_AMD_AWQ_FUSED where it is used (awq_lite); a misspelt value only warns at
+    import, so workflows that never reach the AWQ search are not broken by it."""
+    if _AWQ_FUSED not in _AWQ_FUSED_CHOICES:
+        raise ValueError(f"MTQ_AMD_AWQ_FUSED={_AWQ_FUSED!r}: expected auto, always, library or never")
+
+
+if _AWQ_FUSED not in _AWQ_FUSED_CHOICES:
+    warnings.warn(f"MTQ_AMD_AWQ_FUSED={_AWQ_FUSED!r}: expected auto, always, library or never; "
+                  "awq_lite will raise", stacklevel=1)
 # Budget for keeping every alpha's quantised weight [11, N, K] across the search batches (it does
 # not change between batches; the reference recomputes it per batch): a fraction of the HBM free
 # when the search pass starts (Llama-3-8B: 154 GB of 288 GB).
@@ -707,6 +718,7 @@ def _awq_release_wq_caches():
 @torch.no_grad()
 def awq_lite(model: nn.Module, forward_loop: ForwardLoop, alpha_step: float = 0.1, debug: bool = False, **kwargs):
     """AWQ-lite scale search (reference :1395-1721)."""
+    _check_awq_fused()
     if forward_loop is None:
         warnings.warn("forward_loop must be provided for awq_lite; skipping awq_lite")
         return

@@ -40,3 +40,40 @@ def test_bench_self_launch_propagates_rank_failure():
     p = _run([], {"MTQ_AMD_DIST_BACKEND": "no_such_backend"})
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+
+
+def _c4_single_process():
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, str(REPO / "benchmarks" / "ptq_c4.py"), "--dims", "tiny", "--samples", "16",
+           "--seq", "64", "--batch", "4"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(REPO), env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")][-1])
+
+
+def test_bench_c4_leg_layer_sharded_matches_single_process():
+    """`bench.py --device cpu --gpus N` runs the C4 leg through the
+    layer-sharded path (sharded.py: P2P hand-off between stages, one packed all_reduce(MAX) in
+    sync_sharded_amax) at tiny dims, and every rank ends with the amax state of a single-process
+    calibration bit for bit (sha256 over all quantizers' amax)."""
+    ref = _c4_single_process()
+    assert ref["world"] == 1 and ref["packed_amax_entries"] is None
+    assert ref["quantizers_with_amax"] == ref["enabled_quantizers"] > 0
+    for n in (2, 3):
+        p = subprocess.run(
+            [sys.executable, str(REPO / "bench.py"), "--gpus", str(n), "--no-suite", "--no-cpu", "--device", "cpu",
+             "--steps", "2", "--warmup", "1", "--tokens", "256"],
+            capture_output=True, text=True, timeout=300, cwd=str(REPO),
+            env={**{k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")},
+                 "MTQ_AMD_DIST_BACKEND": "gloo"})
+        assert p.returncode == 0, p.stderr[-2000:]
+        lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+        assert len(lines) == 1, p.stdout
+        c4 = json.loads(lines[0])["ptq_c4"]
+        assert c4["world"] == n and c4["dist_backend"] == "gloo"
+        assert c4["mode"].startswith("layer-sharded")
+        assert c4["stage_layers"] == [0, 2]  # rank 0's stage of the 4 tiny layers
+        assert c4["packed_amax_entries"] >= c4["enabled_quantizers"] > 0
+        assert c4["quantizers_with_amax"] == ref["quantizers_with_amax"]
+        assert c4["amax_sha256"] == ref["amax_sha256"]
+        assert c4["ptq_wall_clock_s"] > 0 and c4["bf16_forward_s"] > 0 and "overhead_frac" in c4

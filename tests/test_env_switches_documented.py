@@ -24,14 +24,23 @@ def test_every_env_switch_is_documented():
     assert documented <= used, sorted(documented - used)
 
 
-def test_awq_fused_switch_validated_at_import():
-    """A misspelt MTQ_AMD_AWQ_FUSED fails at import, not only on the fused search path."""
+def test_awq_fused_switch_validated_at_use():
+    """A misspelt MTQ_AMD_AWQ_FUSED warns at import (FP8 / max-only workflows still import) and
+    makes awq_lite raise, before any calibration work."""
     import os
     import subprocess
     import sys
 
     env = {**os.environ, "MTQ_AMD_AWQ_FUSED": "alwyas",
            "PYTHONPATH": os.pathsep.join([str(REPO / "tensorrt-model-optimizer_amd"), str(REPO)])}
-    r = subprocess.run([sys.executable, "-c", "import modelopt_amd.torch.quantization"], env=env,
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode != 0 and "MTQ_AMD_AWQ_FUSED='alwyas'" in r.stderr, r.stderr[-2000:]
+    code = (
+        "import torch, modelopt_amd.torch.quantization as mtq\n"
+        "m = torch.nn.Linear(64, 64)\n"
+        "mtq.quantize(m, mtq.INT8_DEFAULT_CFG, lambda mm: mm(torch.randn(4, 64)))\n"
+        "print('max ok')\n"
+        "mtq.quantize(torch.nn.Linear(64, 64), mtq.INT4_AWQ_CFG, lambda mm: mm(torch.randn(4, 64)))\n"
+    )
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert "max ok" in r.stdout, r.stderr[-2000:]
+    assert "MTQ_AMD_AWQ_FUSED='alwyas'" in r.stderr  # the import-time warning
+    assert r.returncode != 0 and "ValueError: MTQ_AMD_AWQ_FUSED='alwyas'" in r.stderr, r.stderr[-2000:]

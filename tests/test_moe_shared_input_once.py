@@ -127,3 +127,44 @@ def test_token_separable_nvfp4_needs_a_static_global_amax():
     assert not hf._token_separable(q)
     q.amax = torch.tensor(3.0)
     assert hf._token_separable(q)
+
+
+def test_installed_fused_experts_forward_reads_only_routed_rows(monkeypatch):
+    """Pins the assumption behind the collect-only late path: the installed
+    transformers fused-experts forward (MixtralExperts, eager) feeds its first projection of expert
+    e exactly hidden_states[tokens routed to e] -- no dense product over all tokens -- so a shared
+    input quantizer collected once on hidden_states sees what the per-expert calls would.  If an
+    upstream release changes the loop (e.g. a dense matmul before the gather), this fails."""
+    from transformers import MixtralConfig
+    from transformers.models.mixtral.modeling_mixtral import MixtralExperts
+
+    cfg = MixtralConfig(hidden_size=16, intermediate_size=24, num_local_experts=4, num_experts_per_tok=2)
+    cfg._experts_implementation = "eager"
+    ex = MixtralExperts(cfg)
+    g = torch.Generator().manual_seed(64)
+    with torch.no_grad():
+        ex.gate_up_proj.normal_(0, 0.2, generator=g)
+        ex.down_proj.normal_(0, 0.2, generator=g)
+    hs = torch.randn(12, 16, generator=g)
+    idx = torch.stack([torch.randperm(4, generator=g)[:2] for _ in range(12)])
+    idx[5] = torch.tensor([1, 3])  # expert 0 and 2 skipped by this row
+    wts = torch.rand(12, 2, generator=g)
+    seen = []
+    orig = torch.nn.functional.linear
+
+    def spy(x, w, b=None):
+        seen.append((x, w))
+        return orig(x, w, b)
+
+    monkeypatch.setattr(torch.nn.functional, "linear", spy)
+    with torch.no_grad():
+        ex(hs, idx, wts)
+    first = [(x, w) for x, w in seen if w.shape == ex.gate_up_proj.shape[1:]]
+    assert sum(x.shape[0] for x, _ in first) == idx.numel()  # every (token, k) pair once
+    for x, w in first:
+        e = (w.storage_offset() - ex.gate_up_proj.storage_offset()) // ex.gate_up_proj.stride(0)
+        tok = (idx == e).any(-1).nonzero().flatten()
+        # each row of the gather is one routed token's hidden state (in the loop's own order)
+        src = [int((hs == r).all(-1).nonzero().flatten()[0]) for r in x]
+        assert sorted(src) == tok.tolist(), e
+        assert torch.equal(x, hs[src]), e
