@@ -386,6 +386,19 @@ int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const v
  *    mtq_awq_mse_multi_workspace_floats(n, G) floats; deterministic. */
 int mtq_awq_prescale(const void *x, const void *sinv, void *xs, int64_t M, int64_t K, int dtype, int G,
                      hipStream_t stream);
+/* AWQ-lite scale statistics, bit-identical to the reference's CPU run (csrc/mtq_awq_scale.hip):
+ *  mtq_col_mean: y[k] = float(T(sum_m v[m, k] / M)), v = |x| (absval) or x, row-major [M, K] of
+ *    dtype T (bf16 / f16 / fp32), summed in ATen's CPU order (SumKernel.cpp cascade) -- replaces
+ *    get_act_scale `x.abs().view(-1, K).mean(0).float()` (model_calib.py:1471-1472) and the mean of
+ *    get_weight_scale (:1453-1469).  workspace: mtq_col_mean_workspace_floats(M, K) floats.
+ *  mtq_awq_scale_table: scales[g, :] = get_scale(x_max, w_max, alpha_g) (:1474-1487) for G
+ *    alphas, e_num[g] = alpha_g and e_den[g] = 1 - alpha_g as doubles (device), pow as ATen's CPU
+ *    pow(Tensor, Scalar) computes it. */
+int64_t mtq_col_mean_workspace_floats(int64_t M, int64_t K);
+int mtq_col_mean(const void *x, int64_t M, int64_t K, int dtype, int absval, float *workspace,
+                 int64_t workspace_floats, float *y, hipStream_t stream);
+int mtq_awq_scale_table(const float *x_max, const float *w_max, int64_t K, const double *e_num,
+                        const double *e_den, int G, float *scales, hipStream_t stream);
 int64_t mtq_awq_mse_multi_workspace_floats(int64_t n, int G);
 int mtq_awq_mse_multi(const void *out, const void *ref, int64_t n, int dtype, int G, float *loss,
                       float *workspace, int64_t workspace_floats, hipStream_t stream);

@@ -57,7 +57,7 @@ def build_kernels(force: bool = False) -> Path:
     changed), then one link."""
     out = OUT / "libmtq_amd.so"
     srcs = [CSRC / "mtq_kernels.hip", CSRC / "mtq_search.hip", CSRC / "mtq_qlinear.hip", CSRC / "mtq_awq_gemm.hip",
-            CSRC / "mtq_attention.hip", CSRC / "mtq_cpu.cpp"]
+            CSRC / "mtq_awq_scale.hip", CSRC / "mtq_attention.hip", CSRC / "mtq_cpu.cpp"]
     hdrs = [CSRC / "mtq_device.hpp", INC / "mtq_amd.h"]
     OBJ.mkdir(parents=True, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror=misleading-indentation", "-Wno-unused-function", f"-I{INC}"]

@@ -519,6 +519,50 @@ at::Tensor awq_prescale(const at::Tensor &x, const at::Tensor &sinv) {
   return y;
 }
 
+// y[k] = float(T(sum_m x[m, k] / M)) in ATen's CPU summation order (mtq_col_mean): awq_lite's
+// get_act_scale (absval) and get_weight_scale means, reference model_calib.py:1453-1472
+at::Tensor col_mean(const at::Tensor &x, bool absval) {
+  check_device(x, "x");
+  const int dt = checked_dtype(x, "x");
+  TORCH_CHECK(dt == MTQ_BF16 || dt == MTQ_F16 || dt == MTQ_F32, "col_mean: bf16 / f16 / fp32 only");
+  TORCH_CHECK(x.dim() >= 1, "col_mean: x must have a last dimension");
+  const int64_t K = x.size(-1);
+  at::Tensor xc = x.contiguous().view({-1, K});
+  const int64_t M = xc.size(0);
+  TORCH_CHECK(M >= 1, "col_mean: no rows");
+  at::Tensor y = at::empty({K}, x.options().dtype(at::kFloat));
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t wf = mtq_col_mean_workspace_floats(M, K);
+  at::Tensor ws = at::empty({std::max<int64_t>(wf, 1)}, x.options().dtype(at::kFloat));
+  check_status(mtq_col_mean(xc.data_ptr(), M, K, dt, absval ? 1 : 0, ws.data_ptr<float>(), ws.numel(),
+                            y.data_ptr<float>(), cur_stream(xc)),
+               "col_mean");
+  return y;
+}
+
+// the AWQ get_scale rows of G alphas with the CPU's pow (mtq_awq_scale_table); e_num / e_den are
+// the fp64 exponents alpha and 1 - alpha (reference model_calib.py:1474-1487)
+at::Tensor awq_scale_table(const at::Tensor &x_max, const at::Tensor &w_max, const at::Tensor &e_num,
+                           const at::Tensor &e_den) {
+  check_device(x_max, "x_max");
+  TORCH_CHECK(x_max.scalar_type() == at::kFloat && w_max.scalar_type() == at::kFloat,
+              "awq_scale_table: fp32 act / weight scales");
+  const int64_t K = x_max.numel();
+  TORCH_CHECK(K >= 1 && w_max.numel() == K, "awq_scale_table: act / weight scale sizes differ");
+  TORCH_CHECK(e_num.scalar_type() == at::kDouble && e_den.scalar_type() == at::kDouble &&
+                  e_num.numel() == e_den.numel(),
+              "awq_scale_table: fp64 exponent vectors of equal length");
+  const int64_t G = e_num.numel();
+  at::Tensor xc = x_max.contiguous().view({-1}), wc = w_max.to(x_max.device()).contiguous().view({-1});
+  at::Tensor en = e_num.to(x_max.device()).contiguous(), ed = e_den.to(x_max.device()).contiguous();
+  at::Tensor out = at::empty({G, K}, x_max.options());
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x_max.device());
+  check_status(mtq_awq_scale_table(xc.data_ptr<float>(), wc.data_ptr<float>(), K, en.data_ptr<double>(),
+                                   ed.data_ptr<double>(), (int)G, out.data_ptr<float>(), cur_stream(xc)),
+               "awq_scale_table");
+  return out;
+}
+
 // loss[g] += mean((out[g] - ref)^2) for all g at once (mtq_awq_mse_multi)
 void awq_mse_multi(const at::Tensor &out, const at::Tensor &ref, at::Tensor loss) {
   check_device(out, "out");
@@ -1159,6 +1203,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("block_quant_dynamic_multi(Tensor inputs, Tensor pqs, int block, int num_bits, bool unsigned, "
         "bool narrow_range) -> Tensor");
   m.def("awq_prescale(Tensor x, Tensor sinv) -> Tensor");
+  m.def("col_mean(Tensor x, bool absval) -> Tensor");
+  m.def("awq_scale_table(Tensor x_max, Tensor w_max, Tensor e_num, Tensor e_den) -> Tensor");
   m.def("awq_mse_multi(Tensor out, Tensor ref, Tensor(a!) loss) -> ()");
   m.def("awq_search_gemm(Tensor x, Tensor sinv, Tensor wq, Tensor? bias, Tensor yref, Tensor(a!) loss) -> ()");
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
@@ -1205,6 +1251,8 @@ TORCH_LIBRARY_IMPL(modelopt_amd, CUDA, m) {
   m.impl("mul_cols", &mul_cols);
   m.impl("awq_search_gemm", &awq_search_gemm);
   m.impl("awq_prescale", &awq_prescale);
+  m.impl("col_mean", &col_mean);
+  m.impl("awq_scale_table", &awq_scale_table);
   m.impl("awq_mse_multi", &awq_mse_multi);
   m.impl("block_quant_dynamic_multi", &block_quant_dynamic_multi);
   m.impl("nvfp4_fake_quant_block", &nvfp4_fake_quant_block);

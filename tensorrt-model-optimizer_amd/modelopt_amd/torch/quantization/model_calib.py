@@ -256,12 +256,34 @@ def get_weight_scale(weight, block_size=None):
     scale = scale.view(org_shape)
     if slice_after_padding is not None:
         scale = scale[..., slice_after_padding]
+    if _cpu_order_ok(scale):
+        # the mean in the reference CPU run's summation order (csrc/mtq_awq_scale.hip): torch's
+        # device mean sums in another order and multiplies by 1/N
+        return _ops().col_mean(scale.reshape(-1, scale.shape[-1]), False)
     return scale.mean(0).to(torch.float32)
 
 
 def get_act_scale(x):
     """mean_tokens(|x|) in fp32 (reference :1471-1472)."""
+    if _cpu_order_ok(x):
+        return _ops().col_mean(x, True)  # |x| and the CPU summation order in one pass
     return x.abs().contiguous().view(-1, x.shape[-1]).mean(0).to(torch.float32)
+
+
+def _cpu_order_ok(t) -> bool:
+    """The AWQ statistics of a device tensor go through the kernels that reproduce the reference's
+    CPU operation order bit for bit (mtq_col_mean / mtq_awq_scale_table)."""
+    return (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and t.dim() >= 1 and t.numel() > 0)
+
+
+def _true_div(t: torch.Tensor, n) -> torch.Tensor:
+    """``t / n`` for a Python number ``n`` as the reference's CPU run computes it (a correctly
+    rounded division): torch on the GPU turns a division by a host scalar into a multiplication
+    by its reciprocal, which is 1 ulp off on some elements."""
+    if isinstance(t, torch.Tensor) and t.is_cuda and t.is_floating_point():
+        return t / torch.tensor(n, dtype=t.dtype, device=t.device)
+    return t / n
 
 
 # The linears that read one tensor (q/k/v_proj, gate/up_proj) each take its act scale in the caching
@@ -288,6 +310,12 @@ def _act_scale_memo_clear():
 
 def get_scale(x_max, w_max, alpha, tensor_parallel_group=None):
     """AWQ scale for one alpha (reference :1474-1487)."""
+    if _cpu_order_ok(x_max) and x_max.dtype == torch.float32:
+        scales = _scale_table(x_max, w_max, [alpha])[0]
+        if tensor_parallel_group is not None and tensor_parallel_group.is_initialized():
+            dist.all_reduce(scales, op=dist.ReduceOp.SUM, group=tensor_parallel_group.group)
+            scales /= tensor_parallel_group.world_size()
+        return scales
     scales = (
         (x_max.pow(alpha) / (w_max.to(x_max.device).pow(1 - alpha) + torch.finfo(torch.float32).tiny))
         .clamp(min=1e-4, max=1e4)
@@ -308,6 +336,12 @@ def _scale_table(x_max, w_max, alphas):
     (tests/test_awq_scale_table.py).  The search tables of every linear are built in the first
     search batch, where ~110 small host-issued ops per linear held the GPU back by ~0.6 s."""
     w = w_max.to(x_max.device)
+    if _cpu_order_ok(x_max) and x_max.dtype == torch.float32 and w.dtype == torch.float32:
+        # one launch for every alpha, with the pow of the reference's CPU run (ATen's vectorised
+        # powf and its special exponents, csrc/mtq_awq_scale.hip): bit-identical rows
+        e_num = torch.tensor([float(a) for a in alphas], dtype=torch.float64)
+        e_den = torch.tensor([1 - a for a in alphas], dtype=torch.float64)
+        return _ops().awq_scale_table(x_max.reshape(-1), w.reshape(-1), e_num, e_den)
     num = torch.stack([x_max.pow(a) for a in alphas])
     den = torch.stack([w.pow(1 - a) for a in alphas])
     scales = (num / (den + torch.finfo(torch.float32).tiny)).clamp(min=1e-4, max=1e4)
@@ -622,7 +656,7 @@ def _awq_sync_act_scale(awq_modules):
                     h.is_enabled = False
                     continue
                 module._if_calib = True
-                h.act_scale = h.act_scale / h.num_cache_steps
+                h.act_scale = _true_div(h.act_scale, h.num_cache_steps)
                 if bool(torch.isnan(h.act_scale).any() or torch.isnan(h.weight_scale).any()):
                     h.is_enabled = False
             continue
@@ -632,7 +666,7 @@ def _awq_sync_act_scale(awq_modules):
             k = module.weight.shape[1]
             dev = h.weight_scale.device
             if h.num_cache_steps > 0:
-                a = (h.act_scale / h.num_cache_steps).reshape(-1)
+                a = _true_div(h.act_scale, h.num_cache_steps).reshape(-1)
                 nan = (torch.isnan(a).any() | torch.isnan(h.weight_scale).any()).reshape(1)
                 present = torch.ones(1, device=dev)
             else:
@@ -652,7 +686,7 @@ def _awq_sync_act_scale(awq_modules):
             dtype = h.act_scale.dtype if isinstance(h.act_scale, torch.Tensor) else torch.float32
             # fixed_order_sum_many returns every slice on the first linear's device: back to this
             # linear's (a model spread over several GPUs by device_map)
-            h.act_scale = (a / n_present).to(device=h.weight_scale.device, dtype=dtype)
+            h.act_scale = _true_div(a, n_present).to(device=h.weight_scale.device, dtype=dtype)
             h.dp_group = g
             h._dp_cache_steps = n_present
 
