@@ -186,18 +186,20 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
                               uint32_t *scratch, int64_t scratch_words, const float *accum, int64_t accum_n,
                               float *hist, hipStream_t stream);
 
-/* The skip_zeros chunk boundaries of the call above, computed on the device (no host sync):
- * torch.histc counts the N non-zero elements as at::parallel_for chunks -- T' = min(threads,
- * ceil(N / grain)), chunk = ceil(N / T'), chunk t = non-zero ranks [t * chunk, (t + 1) * chunk)
- * (calib/histogram.py:116-130 -> torch.histc; grain = at::internal::GRAIN_SIZE = 32768) -- and
- * bounds[t] (device int64 [threads + 1]) is the input index of chunk t's first element, n for an
- * empty chunk: pass bounds and `threads` as chunks to mtq_histogram_abs_chunked.  workspace: int32
- * [mtq_histogram_nonzero_bounds_workspace(n)] per-tile counts, contents irrelevant.  bf16 / f16, x
- * 16-byte aligned, n % 8 == 0.  Zero = |x| bit pattern 0 (+0 and -0). */
-int64_t mtq_histogram_nonzero_bounds_workspace(int64_t n);
-int mtq_histogram_nonzero_bounds(const void *x, int64_t n, int dtype, int threads, int64_t grain,
-                                 int32_t *workspace, int64_t workspace_words, int64_t *bounds,
-                                 hipStream_t stream);
+/* torch.histc of the non-zero |x| with skip_zeros (calib/histogram.py:105-130: `x[x != 0]`, then
+ * torch.histc's per-thread fp32 chunk counts), in ONE read of x and no host sync: the N non-zero
+ * elements form at::parallel_for chunks -- T' = min(threads, ceil(N / grain)), chunk = ceil(N / T'),
+ * chunk t = non-zero ranks [t * chunk, (t + 1) * chunk) (grain = at::internal::GRAIN_SIZE =
+ * 32768) -- each counted exactly, clamped at 2^24 and added in chunk order in fp32, + accum[b]
+ * for b < accum_n; hist fp32 [bins].  Zero = |x| bit pattern 0 (+0 and -0); NaN is non-zero (it
+ * takes a rank, no bin).  bf16 / f16, x 16-byte aligned, n % 8 == 0, threads <= 1024, bins <=
+ * 8176 (MTQ_ERR_INVALID_ARG otherwise; n == 0 writes accum / zeros without reading x).  scratch:
+ * uint32 [mtq_histogram_nonzero_scratch_words(n, threads, bins)], contents irrelevant.
+ * Replaces the r05 mtq_histogram_nonzero_bounds (boundaries by a second read of x). */
+int64_t mtq_histogram_nonzero_scratch_words(int64_t n, int threads, int bins);
+int mtq_histogram_abs_nonzero_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
+                                      int threads, int64_t grain, uint32_t *scratch, int64_t scratch_words,
+                                      const float *accum, int64_t accum_n, float *hist, hipStream_t stream);
 
 /* ---- NVFP4 --------------------------------------------------------------------------------
  * Two-level dynamic NVFP4 fake quant of x [rows, cols] (blocks of block_size along cols, zero

@@ -1468,6 +1468,30 @@ struct HistChunks {
   uint32_t *rows;  // [chunks * bpc, bins] per-workgroup counts, overwritten
 };
 
+// NZ (skip_zeros, r06): torch.histc's chunks of the compacted non-zero elements, counted in ONE
+// read of the input.  The chunk boundaries depend on the non-zero count of everything before
+// them, so the counting launch cannot know them; it counts uniform, slab-aligned workgroup ranges
+// instead, storing per workgroup its bin row, its non-zero count and the non-zero count of each
+// slab (one 2048-vector batch of its count loop, counted by wave ballots: no LDS traffic), and
+// zeroes the boundary rows.  A boundary that falls strictly inside a workgroup's range is then
+// resolved by hist_nz_recount_kernel: one workgroup per (boundary, slab) re-reads only the slabs
+// of that range which hold non-zeros of the boundary's chunk-before segment (at most one
+// workgroup range per boundary, ~1.5 % of the input at 16 threads) and adds their bins into
+// rec[b]; hist_nz_fold_kernel assembles chunk c from whole rows, rec[c + 1] (its part of the
+// workgroup its end cuts) and row - sum rec (its part of the workgroup its start cuts) -- all
+// exact uint32 -- then clamps and adds the chunks in order as the CHUNKED fold does.  Replaces
+// the r05 per-tile non-zero pass + per-boundary block scans (a second full read of the input).
+struct HistNz {
+  int64_t vpb;         // vectors per workgroup range (a multiple of the slab)
+  int S;               // slabs per workgroup range
+  uint32_t *rows;      // [G, bins]
+  uint32_t *wg_tot;    // [G] non-zero elements per workgroup range
+  uint32_t *slab_tot;  // [G, S] non-zero elements per slab
+  uint32_t *rec;       // [threads, bins] boundary segment counts (zeroed by the count launch)
+  int64_t rec_words;
+};
+constexpr int kHvCounts = 0, kHvChunked = 1, kHvNz = 2;
+
 // workgroups per chunk of the chunked count: ~one 1024-thread workgroup per CU in total, at
 // least kHistValThreads * 8 vectors each
 int64_t hist_chunk_bpc(int64_t n, int chunks) {
@@ -1520,10 +1544,11 @@ __global__ __launch_bounds__(BW * 16) void hist_fold_blocks_kernel(const uint32_
   }
 }
 
-template <typename T, int U, bool CHUNKED = false>
+template <typename T, int U, int MODE = kHvCounts>
 __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
     const T *__restrict__ x, int64_t nvec, int64_t vec_per_block, const float *hmax, int bins,
-    int skip_zeros, uint32_t *counts, HistChunks ch) {
+    int skip_zeros, uint32_t *counts, HistChunks ch, HistNz nz) {
+  constexpr bool CHUNKED = MODE == kHvChunked;
   static_assert(sizeof(T) == 2, "pattern histogram is for 16-bit floats");
   extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
   uint32_t *vh = sh;                  // [32768] counts per |x| bit pattern
@@ -1553,6 +1578,7 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
     v1 = v1 < cv1 ? v1 : cv1;
     v0 = v0 < v1 ? v0 : v1;
   } else {
+    if constexpr (MODE == kHvNz) vec_per_block = nz.vpb;
     v0 = (int64_t)blockIdx.x * vec_per_block;
     v1 = v0 + vec_per_block;
     v1 = v1 < nvec ? v1 : nvec;
@@ -1609,18 +1635,53 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   for (int k = threadIdx.x; k < nz4; k += kHistValThreads)
     reinterpret_cast<uint4 *>(vh)[k] = make_uint4(0u, 0u, 0u, 0u);
   for (int k = threadIdx.x; k < bins; k += kHistValThreads) bh[k] = 0;
+  uint32_t *slab_w = bh + bins;  // [S][16] per-wave non-zero counts of each slab (kHvNz)
+  const int wave = threadIdx.x >> 6;
+  if constexpr (MODE == kHvNz) {
+    // this workgroup's share of the boundary rows, zeroed for the recount launch
+    const int64_t per = (nz.rec_words + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * per;
+    for (int64_t k = r0 + threadIdx.x; k < r0 + per && k < nz.rec_words; k += kHistValThreads) nz.rec[k] = 0u;
+  }
   __syncthreads();  // LDS zeroed (the first batch's loads issued before)
   // (no branch around B's count either: with one, the compiler sank B's loads into it and waited
   // vmcnt(0) right behind them; a past-the-end B batch costs its lanes' dummy atomics instead)
-  for (; i < v1; i += 2 * kStep) {
+  // kHvNz: a slab = one batch (kStep vectors, contiguous); the wave's non-zero halves of a batch
+  // by ballots (wave-uniform, SALU popcounts), kept in lane `slab` of one VGPR (a lane select: no
+  // LDS write and no branch in the loop -- a lane-0-only LDS write split the loop body and the
+  // scheduler then waited vmcnt(0) for batch B before issuing the next A loads); S <= 64
+  uint32_t slab_acc = 0u;
+  auto slab_count = [&](const u32x4 *v, int64_t ib, int slab) {
+    if constexpr (MODE == kHvNz) {
+      int c = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t okm = __ballot(ib + (int64_t)u * kHistValThreads < v1);
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t m = w[j] & 0x7FFF7FFFu;
+          c += __popcll(__ballot((m & 0xFFFFu) != 0u) & okm);
+          c += __popcll(__ballot(m > 0xFFFFu) & okm);
+        }
+      }
+      slab_acc = (int)(threadIdx.x & 63) == slab ? (uint32_t)c : slab_acc;  // v_cmp + v_cndmask
+    }
+  };
+  for (int it = 0; i < v1; i += 2 * kStep, ++it) {
 #pragma unroll
     for (int u = 0; u < U; ++u) b[u] = ld(i + kStep + (int64_t)u * kHistValThreads);
 #pragma unroll
     for (int u = 0; u < U; ++u) count(a[u], i + (int64_t)u * kHistValThreads < v1);
+    slab_count(a, i, 2 * it);
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = ld(i + 2 * kStep + (int64_t)u * kHistValThreads);
 #pragma unroll
     for (int u = 0; u < U; ++u) count(b[u], i + kStep + (int64_t)u * kHistValThreads < v1);
+    slab_count(b, i + kStep, (2 * it + 1) & 63);  // a past-the-range B batch counts 0 (written, unread)
+  }
+  if constexpr (MODE == kHvNz) {
+    if ((threadIdx.x & 63) < nz.S) slab_w[(threadIdx.x & 63) * 16 + wave] = slab_acc;
   }
   if constexpr (CHUNKED) {
     if (blockIdx.x % ch.bpc == 0 && threadIdx.x == 0 && e1 > e0) {
@@ -1679,25 +1740,34 @@ __global__ __launch_bounds__(kHistValThreads) void hist_value_kernel(
   if constexpr (CHUNKED) {
     uint32_t *row = ch.rows + (int64_t)blockIdx.x * bins;
     for (int b = threadIdx.x; b < bins; b += kHistValThreads) __builtin_nontemporal_store(bh[b], row + b);
+  } else if constexpr (MODE == kHvNz) {
+    uint32_t *row = nz.rows + (int64_t)blockIdx.x * bins;
+    for (int b = threadIdx.x; b < bins; b += kHistValThreads) __builtin_nontemporal_store(bh[b], row + b);
+    // slab totals, and the workgroup's total through one LDS word (the pattern table is free now)
+    if (threadIdx.x == 0) vh[0] = 0u;
+    __syncthreads();
+    for (int k = threadIdx.x; k < nz.S; k += kHistValThreads) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w2 = 0; w2 < 16; ++w2) t += slab_w[k * 16 + w2];
+      nz.slab_tot[(int64_t)blockIdx.x * nz.S + k] = t;
+      atomicAdd(vh, t);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) nz.wg_tot[blockIdx.x] = vh[0];
   } else {
     for (int b = threadIdx.x; b < bins; b += kHistValThreads)
       if (bh[b]) atomicAdd(counts + b, bh[b]);
   }
 }
 
-// skip_zeros chunk boundaries on the device (replaces an int64 cumsum over the whole input, a
-// host sync on its last element and a searchsorted; r05b: 1.25 ms for bf16 [8192, 14336]).
-// torch.histc counts the compacted non-zero elements, N of them, as at::parallel_for chunks:
-// T' = min(T, ceil(N / grain)) threads, chunk = ceil(N / T'), chunk t = compacted ranks
-// [t * chunk, (t + 1) * chunk).  Its first element in the input is bounds[t]; chunks at or past
-// N are empty (bounds = n).
-//   1. hist_nz_tiles_kernel: non-zero |x| count per tile of kNzTileVec vectors (one read of x);
-//   2. hist_nz_bounds_kernel: block t sums the tile counts (N), finds the tile holding rank
-//      t * chunk by a block scan of the tile counts, then the element by a block scan of that
-//      tile's per-lane counts -- T + 1 blocks, ~2 tiles' reads in total.
+// skip_zeros: torch.histc counts the compacted non-zero elements, N of them, as
+// at::parallel_for chunks: T' = min(T, ceil(N / grain)) threads, chunk = ceil(N / T'), chunk t =
+// compacted ranks [t * chunk, (t + 1) * chunk).  r05 found the chunks' first elements on the
+// device with a per-tile non-zero pass and one block per boundary (a second full read of the
+// input, plus T + 1 blocks each re-summing every tile count); r06 counts in one read (kHvNz
+// above) and resolves the boundaries afterwards (hist_nz_recount_kernel, hist_nz_fold_kernel).
 constexpr int kNzThreads = 1024;
-constexpr int kNzPerLane = 8;                            // vectors per lane
-constexpr int64_t kNzTileVec = (int64_t)kNzThreads * kNzPerLane;  // 8192 vectors = 65536 elements
 
 __device__ __forceinline__ int nz_halves(uint32_t w) {
   return ((w & 0x7FFFu) != 0u) + ((w & 0x7FFF0000u) != 0u);
@@ -1728,97 +1798,246 @@ __device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t *sh_w, int64_
   return base + inc - v;
 }
 
-__global__ __launch_bounds__(kNzThreads) void hist_nz_tiles_kernel(const u32x4 *__restrict__ x, int64_t nvec,
-                                                                   int32_t *__restrict__ tiles) {
-  const int64_t t0 = (int64_t)blockIdx.x * kNzTileVec;
-  // every load issued before the first count (clamped, then masked; under the lane condition the
-  // compiler waited vmcnt(0) behind each)
-  u32x4 v[kNzPerLane];
-#pragma unroll
-  for (int u = 0; u < kNzPerLane; ++u) {
-    const int64_t i = t0 + (int64_t)u * kNzThreads + threadIdx.x;
-    v[u] = __builtin_nontemporal_load(x + (i < nvec ? i : nvec - 1));
-  }
-  int c = 0;
-#pragma unroll
-  for (int u = 0; u < kNzPerLane; ++u)
-    if (t0 + (int64_t)u * kNzThreads + threadIdx.x < nvec) c += nz_vec(v[u]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  __shared__ int sw[kNzThreads / 64];
-  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-#pragma unroll
-    for (int k = 0; k < kNzThreads / 64; ++k) t += sw[k];
-    tiles[blockIdx.x] = t;
-  }
-}
-
-__global__ __launch_bounds__(kNzThreads) void hist_nz_bounds_kernel(const u32x4 *__restrict__ x, int64_t nvec,
-                                                                    const int32_t *__restrict__ tiles,
-                                                                    int64_t ntiles, int threads, int64_t grain,
-                                                                    int64_t *__restrict__ bounds) {
-  __shared__ int64_t sh_w[kNzThreads / 64];
-  __shared__ int64_t sh_tile, sh_rem;
-  const int t = blockIdx.x;
-  const int64_t n = nvec * 8;
-  // tile counts: lane l owns the contiguous slice [l * per, (l + 1) * per)
-  const int64_t per = (ntiles + kNzThreads - 1) / kNzThreads;
-  const int64_t s0 = (int64_t)threadIdx.x * per;
+// hist_nz_recount_kernel: grid (threads - 1) x S, workgroup (b - 1, p) = boundary b, slab p of
+// the workgroup range that boundary b falls strictly inside (nothing to do otherwise).  The chunks
+// are torch.histc's: N non-zeros (sum of wg_tot), T' = min(threads, ceil(N / grain)), chunk =
+// ceil(N / T'), boundary b at compacted rank b * chunk.  Its segment is the non-zeros of that
+// workgroup range with ranks in [max(R_w, (b - 1) * chunk), b * chunk) -- the part the range gives
+// to chunk b - 1 -- and this workgroup adds the ones in slab p to rec[b].
+// int64 block-prefix of the uint32 array v[0, n) into pre[0, n] (pre[n] = total), 1024 threads;
+// each thread's contiguous slice is loaded 8 at a time, all 8 loads issued together (one round
+// trip for n <= 8192 -- a plain loop over the slice waited for each load in turn, r06j)
+__device__ void block_prefix_u32(const uint32_t *v, int64_t n, int64_t *pre, int64_t *sh_w) {
+  const int64_t per = (n + kNzThreads - 1) / kNzThreads;
+  const int64_t s0 = (int64_t)threadIdx.x * per, s1 = s0 + per < n ? s0 + per : n;
   int64_t mine = 0;
-  for (int64_t k = s0; k < s0 + per && k < ntiles; ++k) mine += tiles[k];
-  int64_t kept;
-  const int64_t before = block_exscan(mine, sh_w, &kept);
-  const int64_t tq = (kept + grain - 1) / grain;
-  const int64_t teff = (int64_t)threads < tq ? (int64_t)threads : tq;  // 0 when kept == 0
-  const int64_t chunk = teff > 0 ? (kept + teff - 1) / teff : 1;
-  const int64_t target = (int64_t)t * chunk;  // compacted rank of chunk t's first element
-  if (t == 0 || target >= kept) {
-    if (threadIdx.x == 0) bounds[t] = t == 0 ? 0 : n;
-    return;  // block-uniform
-  }
-  if (threadIdx.x == 0) sh_tile = -1;
-  __syncthreads();
-  if (before <= target && target < before + mine) {  // exactly one lane
-    int64_t acc = before, k = s0;
-    while (acc + tiles[k] <= target) acc += tiles[k++];
-    sh_tile = k;
-    sh_rem = target - acc;
-  }
-  __syncthreads();
-  const int64_t tile = sh_tile, rem = sh_rem;
-  // the tile's vectors: lane l owns [v0 + l * 8, + 8) (contiguous, so ranks follow lane order)
-  const int64_t v0 = tile * kNzTileVec + (int64_t)threadIdx.x * kNzPerLane;
-  // all eight loads issued before the first is used (clamped, then masked: a load under the lane
-  // condition made the compiler wait for each one in turn)
-  u32x4 v[kNzPerLane];
+  for (int64_t k0 = s0; k0 < s1; k0 += 8) {
+    uint32_t t[8];
 #pragma unroll
-  for (int u = 0; u < kNzPerLane; ++u) v[u] = x[v0 + u < nvec ? v0 + u : nvec - 1];
-  int c = 0;
+    for (int k = 0; k < 8; ++k) t[k] = v[k0 + k < s1 ? k0 + k : s1 - 1];
 #pragma unroll
-  for (int u = 0; u < kNzPerLane; ++u) {
-    if (v0 + u >= nvec) v[u] = u32x4{0u, 0u, 0u, 0u};
-    c += nz_vec(v[u]);
-  }
-  int64_t tot;
-  const int64_t lb = block_exscan(c, sh_w, &tot);
-  if (lb <= rem && rem < lb + c) {  // exactly one lane holds the rem-th non-zero of the tile
-    int64_t r = rem - lb;
-#pragma unroll
-    for (int u = 0; u < kNzPerLane; ++u) {
-      const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const bool nz = (w4[h / 2] >> (16 * (h % 2)) & 0x7FFFu) != 0u;
-        if (nz) {
-          if (r == 0) bounds[t] = (v0 + u) * 8 + h;
-          --r;
-        }
+    for (int k = 0; k < 8; ++k) {
+      if (k0 + k < s1) {
+        pre[k0 + k] = mine;  // exclusive within the slice; the slice offset is added below
+        mine += t[k];
       }
     }
   }
+  int64_t tot;
+  const int64_t off = block_exscan(mine, sh_w, &tot);
+  for (int64_t k = s0; k < s1; ++k) pre[k] += off;
+  if (threadIdx.x == 0) pre[n] = tot;
+  __syncthreads();
+}
+
+struct NzChunking {
+  int64_t N, teff, chunk;
+  double inv;  // 1 / chunk, for chunk_of
+};
+
+// floor(r / chunk) without a 64-bit integer division (a ~100-instruction sequence on the GPU: the
+// fold ran 15 us with two per workgroup range and lane, r06k): the double quotient is within one
+// of it for r < 2^50, corrected by one multiply-compare each way
+__device__ __forceinline__ int64_t chunk_of(int64_t r, const NzChunking &c) {
+  int64_t q = (int64_t)((double)r * c.inv);
+  if (q * c.chunk > r) --q;
+  else if ((q + 1) * c.chunk <= r) ++q;
+  return q;
+}
+
+__device__ __forceinline__ NzChunking nz_chunking(int64_t N, int threads, int64_t grain) {
+  NzChunking c;
+  c.N = N;
+  const int64_t tq = (N + grain - 1) / grain;
+  c.teff = (int64_t)threads < tq ? (int64_t)threads : tq;  // 0 when N == 0
+  c.chunk = c.teff > 0 ? (N + c.teff - 1) / c.teff : 1;
+  c.inv = 1.0 / (double)c.chunk;
+  return c;
+}
+
+constexpr int kNzSlabVec = (int)kHistValThreads * 2;  // the count kernel's batch (U = 2)
+
+template <typename T>
+__global__ __launch_bounds__(kNzThreads) void hist_nz_recount_kernel(const u32x4 *__restrict__ x, int64_t nvec,
+                                                                      HistNz nz, int G, int threads, int64_t grain,
+                                                                      const float *hmax, int bins) {
+  extern __shared__ __attribute__((aligned(16))) int64_t shq[];
+  int64_t *R = shq;                    // [G + 1] workgroup rank prefix
+  int64_t *Rs = R + G + 1;             // [S + 1] slab rank prefix inside the boundary's workgroup
+  int64_t *sh_w = Rs + nz.S + 1;       // [16] scan scratch
+  int64_t *sh_misc = sh_w + 16;        // [2]
+  uint32_t *bh = reinterpret_cast<uint32_t *>(sh_misc + 2);  // [bins]
+  const int b = blockIdx.x + 1, p = blockIdx.y;
+  block_prefix_u32(nz.wg_tot, G, R, sh_w);
+  const NzChunking ck = nz_chunking(R[G], threads, grain);
+  const int64_t target = (int64_t)b * ck.chunk;
+  if (b >= ck.teff || target >= ck.N) return;  // block-uniform
+  if (threadIdx.x == 0) sh_misc[0] = -1;
+  __syncthreads();
+  for (int w = threadIdx.x; w < G; w += kNzThreads)
+    if (R[w] < target && target < R[w + 1]) sh_misc[0] = w;  // at most one
+  __syncthreads();
+  const int64_t w = sh_misc[0];
+  if (w < 0 || p >= nz.S) return;  // the boundary sits on a workgroup edge: no split
+  const int64_t rw = R[w];
+  const int64_t rank_lo = rw > target - ck.chunk ? rw : target - ck.chunk, rank_hi = target;
+  block_prefix_u32(nz.slab_tot + w * nz.S, nz.S, Rs, sh_w);
+  const int64_t s_lo = rw + Rs[p], s_hi = rw + Rs[p + 1];
+  if (s_hi <= rank_lo || s_lo >= rank_hi) return;  // no rank of the segment in this slab
+  for (int k = threadIdx.x; k < bins; k += kNzThreads) bh[k] = 0u;
+  // the slab: vectors [v0, v1); lane l takes vectors v0 + 2l, + 1 (contiguous: ranks in lane order)
+  const int64_t v0 = w * nz.vpb + (int64_t)p * kNzSlabVec;
+  int64_t v1 = v0 + kNzSlabVec < (w + 1) * nz.vpb ? v0 + kNzSlabVec : (w + 1) * nz.vpb;
+  v1 = v1 < nvec ? v1 : nvec;
+  u32x4 v[2];
+  int c = 0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t k = v0 + 2 * (int64_t)threadIdx.x + u;
+    v[u] = k < v1 ? x[k] : u32x4{0u, 0u, 0u, 0u};
+    c += nz_vec(v[u]);
+  }
+  int64_t tot;
+  int64_t rank = s_lo + block_exscan(c, sh_w, &tot);  // also orders the bh zeroing before the adds
+  float lo = 0.f, hi = *hmax;
+  if (hi == lo) {
+    lo -= 1.f;
+    hi += 1.f;
+  }
+  const float fb = (float)bins, span = hi - lo, y = 1.f / span;
+  const uint32_t last = (uint32_t)bins - 1u;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const uint16_t bits = (uint16_t)((w4[h / 2] >> (16 * (h % 2))) & 0x7FFFu);
+      if (bits == 0) continue;
+      const bool in = rank >= rank_lo && rank < rank_hi;
+      ++rank;
+      T tv;
+      __builtin_memcpy(&tv, &bits, 2);
+      const float a = Elem<T>::ld(tv);
+      if (!in || !(a <= hi)) continue;  // NaN fails the compare
+      const float t = (a - lo) * fb;
+      const float q0 = t * y;
+      const float q = __builtin_fmaf(__builtin_fmaf(-q0, span, t), y, q0);
+      uint32_t bn = (uint32_t)(int)q;
+      bn = bn < last ? bn : last;
+      atomicAdd(bh + bn, 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t *rec = nz.rec + (int64_t)b * bins;
+  for (int k = threadIdx.x; k < bins; k += kNzThreads)
+    if (bh[k]) atomicAdd(rec + k, bh[k]);
+}
+
+// hist_nz_fold_kernel: BW bins x 16 lanes per workgroup; lane l of bin b loads the rows of
+// workgroup ranges l, l + 16, ... for b -- issued first, together with the boundary rows, before
+// the rank prefix is known, so the whole fold is one round trip -- then adds each range's part
+// into LDS chunk accumulators (uint32, exact): a range inside one chunk gives its whole row; one
+// that boundaries cut gives rec[c + 1] to every chunk c its ranks leave (the segment before the
+// boundary) and row - sum of those to its last chunk.  Chunks in groups of 16: clamp at 2^24 and
+// add in chunk order in fp32 (torch.histc's thread-order fold), + accum.
+constexpr int kNzFoldMaxRec = 16;  // boundary rows staged in LDS per chunk group
+
+template <int BW>
+__global__ __launch_bounds__(BW * 16) void hist_nz_fold_kernel(HistNz nz, int G, int threads, int64_t grain,
+                                                               int bins, const float *accum, int64_t accum_n,
+                                                               float *hist) {  // accum may alias hist
+  extern __shared__ __attribute__((aligned(16))) int64_t shq[];
+  int64_t *R = shq;                                             // [G + 1]
+  int64_t *sh_w = R + G + 1;                                    // [16]
+  int64_t *cfl = sh_w + 16;                                     // [G][2] first / last chunk of each range
+  uint32_t *acc = reinterpret_cast<uint32_t *>(cfl + 2 * G);    // [16][BW]
+  uint32_t *recl = acc + 16 * BW;                               // [kNzFoldMaxRec][BW]
+  const int bl = threadIdx.x % BW, gl = threadIdx.x / BW, bn = blockIdx.x * BW + bl;
+  const int bnc = bn < bins ? bn : bins - 1;
+  // this lane's rows (G <= 256 in one batch of 16 loads; more in further batches below)
+  uint32_t v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int w = gl + 16 * k < G ? gl + 16 * k : G - 1;
+    v[k] = nz.rows[(int64_t)w * bins + bnc];
+  }
+  // the first group's boundary rows (rec[1 .. 16]) and the range totals, loaded beside the rows:
+  // the whole fold waits for one round trip (the totals' scan after the rows' loads made it two)
+  const int nrec0 = threads - 1 < 16 ? threads - 1 : 16;
+  const uint32_t rec0 = nz.rec[(int64_t)(gl < nrec0 ? gl + 1 : 1) * bins + bnc];
+  if (G <= BW * 16) {
+    const uint32_t tot = nz.wg_tot[threadIdx.x < G ? threadIdx.x : G - 1];
+    if (gl < nrec0) recl[gl * BW + bl] = rec0;
+    int64_t all;
+    const int64_t ex = block_exscan(threadIdx.x < G ? tot : 0u, sh_w, &all);
+    if (threadIdx.x < G) R[threadIdx.x] = ex;
+    if (threadIdx.x == 0) R[G] = all;
+    __syncthreads();
+  } else {
+    if (gl < nrec0) recl[gl * BW + bl] = rec0;
+    block_prefix_u32(nz.wg_tot, G, R, sh_w);  // also orders the recl stores before their reads
+  }
+  const NzChunking ck = nz_chunking(R[G], threads, grain);
+  // each range's first / last chunk once per workgroup (the same for every bin; -1: no non-zeros)
+  for (int w = threadIdx.x; w < G; w += BW * 16) {
+    const int64_t rw = R[w], rz = R[w + 1];
+    cfl[2 * w] = rz == rw ? -1 : chunk_of(rw, ck);
+    cfl[2 * w + 1] = rz == rw ? -1 : chunk_of(rz - 1, ck);
+  }
+  float h = 0.f;
+  for (int64_t g0 = 0; g0 < ck.teff; g0 += 16) {
+    const int64_t g1 = g0 + 16 < ck.teff ? g0 + 16 : ck.teff;
+    acc[gl * BW + bl] = 0u;
+    // boundary rows g0 + 1 .. g1 (rec[c + 1] for the group's chunks), staged in LDS slot (c - g0)
+    if (g0 > 0 && g0 + gl + 1 < ck.teff) recl[gl * BW + bl] = nz.rec[(g0 + gl + 1) * bins + bnc];
+    __syncthreads();
+    for (int w0 = 0; w0 < G; w0 += 256) {
+      uint32_t vv[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (w0 == 0) {
+          vv[k] = v[k];
+        } else {
+          const int w = w0 + gl + 16 * k < G ? w0 + gl + 16 * k : G - 1;
+          vv[k] = nz.rows[(int64_t)w * bins + bnc];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int w = w0 + gl + 16 * k;
+        if (w >= G) break;
+        const int64_t cf = cfl[2 * w], cl = cfl[2 * w + 1];  // first / last chunk of its ranks
+        if (cf < 0 || cl < g0 || cf >= g1) continue;  // no non-zeros (an all-zero row), or another group
+        if (cf == cl) {
+          atomicAdd(acc + (cf - g0) * BW + bl, vv[k]);
+          continue;
+        }
+        uint32_t rest = vv[k];
+        for (int64_t c = cf; c < cl; ++c) {  // the segment before boundary c + 1 goes to chunk c
+          const int64_t j = c + 1 - g0 - 1;  // slot of rec[c + 1] when staged (c in the group)
+          const uint32_t r = (c >= g0 && c < g1 && c + 1 <= g0 + 16) ? recl[j * BW + bl]
+                                                                    : nz.rec[(c + 1) * bins + bnc];
+          rest -= r;
+          if (c >= g0 && c < g1) atomicAdd(acc + (c - g0) * BW + bl, r);
+        }
+        if (cl < g1) atomicAdd(acc + (cl - g0) * BW + bl, rest);
+      }
+    }
+    __syncthreads();
+    if (gl == 0 && bn < bins)
+      for (int64_t c = g0; c < g1; ++c) h += fminf((float)acc[(c - g0) * BW + bl], 16777216.f);
+    __syncthreads();
+  }
+  if (gl == 0 && bn < bins) {
+    if (bn < accum_n) h += accum[bn];
+    hist[bn] = h;
+  }
+}
+
+// hist[b] = accum[b] (b < accum_n) or 0: an empty call's result
+__global__ void hist_fill_kernel(const float *accum, int64_t accum_n, int bins, float *hist) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < bins) hist[b] = b < accum_n ? accum[b] : 0.f;
 }
 
 // ============================================================================================
@@ -2989,7 +3208,7 @@ void count_dispatch(int id) { g_dispatch[id].fetch_add(1, std::memory_order_rela
 static const char *const kDispatchNames[kDispCount] = {
     "ew_vec", "ew_group_sk", "ew_group", "ew_rowwave", "amax_persist", "amax_rows_u", "amax_rows_short",
     "amax_cols_wide", "block_quant_dyn", "hist_value", "hist_value_chunked", "mx_vec", "mx_e2m1_native",
-    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_nz_bounds", "mx_e4m3_native"};
+    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_value_nz", "mx_e4m3_native"};
 }  // namespace mtq
 
 // ============================================================================================
@@ -3243,7 +3462,7 @@ int mtq_histogram_abs(const void *x, int64_t n, int dtype, const float *hmax, in
         }
         count_dispatch(kDispHistValue);
         kern<<<(unsigned)blocks, kHistValThreads, shr, stream>>>(xt, nvec, vpb, hmax, bins, skip_zeros, counts,
-                                                                    HistChunks{});
+                                                                    HistChunks{}, HistNz{});
         return check_launch();
       }
     }
@@ -3296,6 +3515,10 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
   if (accum_n < 0 || accum_n > bins || (accum_n > 0 && !accum)) return MTQ_ERR_INVALID_ARG;
   if (!bounds && (chunk_elems < 1 || (chunks - 1) * chunk_elems >= n)) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
+  if (n == 0) {  // nothing to count: no launch may read x
+    hist_fill_kernel<<<(unsigned)((bins + 255) / 256), 256, 0, stream>>>(accum, accum_n, bins, hist);
+    return check_launch();
+  }
   if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
   const int64_t bpc = hist_chunk_bpc(n, chunks);
   if ((int64_t)chunks * bpc > INT32_MAX || scratch_words < (int64_t)chunks * bpc * bins) return MTQ_ERR_INVALID_ARG;
@@ -3303,7 +3526,7 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
     using T = decltype(t);
     if constexpr (sizeof(T) == 2) {
       const size_t shr = ((size_t)kHistPatterns + (size_t)bins) * 4;
-      auto kern = hist_value_kernel<T, 2, true>;
+      auto kern = hist_value_kernel<T, 2, kHvChunked>;
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -3313,7 +3536,7 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
       const HistChunks ch{bounds, chunk_elems, n, (int)bpc, chunks, scratch};
       count_dispatch(kDispHistValueChunked);
       kern<<<(unsigned)(chunks * bpc), kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), n / 8, 0,
-                                                                      hmax, bins, skip_zeros, nullptr, ch);
+                                                                      hmax, bins, skip_zeros, nullptr, ch, HistNz{});
       // 64 bins x 16 chunks per 1024-thread workgroup (16 x 16 per 256 threads: 4.99 vs 4.75-4.90 us
       // in the kernel trace, r05)
       constexpr int kFoldBW = 64;
@@ -3325,26 +3548,102 @@ int mtq_histogram_abs_chunked(const void *x, int64_t n, int dtype, const float *
   });
 }
 
-int64_t mtq_histogram_nonzero_bounds_workspace(int64_t n) {
-  if (n < 0) return -1;
-  return (n / 8 + kNzTileVec - 1) / kNzTileVec;
+// kHvNz geometry: ~one 1024-thread workgroup per CU over slab-aligned ranges; more workgroups
+// only when a range would hold more slabs than the count kernel's LDS takes (> 1.6 G elements)
+struct NzGeom {
+  int64_t vpb;
+  int G, S;
+};
+// LDS of the count kernel: 128 KiB pattern table + the bins + 16 words per slab <= 160 KiB
+constexpr int64_t kNzLdsWords = 160 * 1024 / 4 - kHistPatterns;
+
+NzGeom nz_geom(int64_t nvec, int bins) {
+  int64_t kNzMaxSlabs = (kNzLdsWords - bins) / 16;
+  kNzMaxSlabs = kNzMaxSlabs < 64 ? kNzMaxSlabs : 64;  // one slab per lane of the count kernel's VGPR
+  NzGeom g;
+  int64_t G = num_cus();
+  int64_t slabs = (nvec + kNzSlabVec - 1) / kNzSlabVec;
+  if (slabs < 1) slabs = 1;
+  if (G > slabs) G = slabs;
+  int64_t S = (slabs + G - 1) / G;
+  if (S > kNzMaxSlabs) {
+    S = kNzMaxSlabs;
+    G = (slabs + S - 1) / S;
+  }
+  g.S = (int)S;
+  g.vpb = S * kNzSlabVec;
+  g.G = (int)((nvec + g.vpb - 1) / g.vpb);
+  if (g.G < 1) g.G = 1;
+  return g;
 }
 
-int mtq_histogram_nonzero_bounds(const void *x, int64_t n, int dtype, int threads, int64_t grain,
-                                 int32_t *workspace, int64_t workspace_words, int64_t *bounds,
-                                 hipStream_t stream) {
-  if (n < 0 || threads < 1 || grain < 1 || !bounds || (n > 0 && (!x || !workspace))) return MTQ_ERR_INVALID_ARG;
+// the recount and fold kernels keep the workgroup ranks' prefix in LDS (int64 each)
+size_t nz_recount_lds(const NzGeom &g, int bins) { return (size_t)(g.G + 1 + g.S + 1 + 18) * 8 + (size_t)bins * 4; }
+
+int64_t mtq_histogram_nonzero_scratch_words(int64_t n, int threads, int bins) {
+  if (n < 0 || threads < 1 || threads > 1024 || bins < 1 || bins > kNzLdsWords - 16) return -1;
+  const NzGeom g = nz_geom(n / 8, bins);
+  if (nz_recount_lds(g, bins) > 64 * 1024) return -1;  // > ~6e10 elements: the caller's per-chunk path
+  return (int64_t)g.G * bins + g.G + (int64_t)g.G * g.S + (int64_t)threads * bins;
+}
+
+int mtq_histogram_abs_nonzero_chunked(const void *x, int64_t n, int dtype, const float *hmax, int bins,
+                                      int threads, int64_t grain, uint32_t *scratch, int64_t scratch_words,
+                                      const float *accum, int64_t accum_n, float *hist, hipStream_t stream) {
+  if (n < 0 || bins < 1 || bins > kNzLdsWords - 16 || threads < 1 || threads > 1024 || grain < 1 || !hmax || !hist ||
+      (n > 0 && (!x || !scratch)))
+    return MTQ_ERR_INVALID_ARG;
+  if (accum_n < 0 || accum_n > bins || (accum_n > 0 && !accum)) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
+  if (n == 0) {  // nothing to count (no launch may read x)
+    hist_fill_kernel<<<(unsigned)((bins + 255) / 256), 256, 0, stream>>>(accum, accum_n, bins, hist);
+    return check_launch();
+  }
   if (!aligned16(x) || n % 8 != 0) return MTQ_ERR_INVALID_ARG;
-  const int64_t nvec = n / 8, ntiles = mtq_histogram_nonzero_bounds_workspace(n);
-  if (workspace_words < ntiles) return MTQ_ERR_INVALID_ARG;
-  if (ntiles > 0)
-    hist_nz_tiles_kernel<<<(unsigned)ntiles, kNzThreads, 0, stream>>>(reinterpret_cast<const u32x4 *>(x), nvec,
-                                                                      workspace);
-  count_dispatch(kDispHistNzBounds);
-  hist_nz_bounds_kernel<<<(unsigned)(threads + 1), kNzThreads, 0, stream>>>(
-      reinterpret_cast<const u32x4 *>(x), nvec, workspace, ntiles, threads, grain, bounds);
-  return check_launch();
+  if (scratch_words < mtq_histogram_nonzero_scratch_words(n, threads, bins)) return MTQ_ERR_INVALID_ARG;
+  const int64_t nvec = n / 8;
+  const NzGeom g = nz_geom(nvec, bins);
+  HistNz nz;
+  nz.vpb = g.vpb;
+  nz.S = g.S;
+  nz.rows = scratch;
+  nz.wg_tot = nz.rows + (int64_t)g.G * bins;
+  nz.slab_tot = nz.wg_tot + g.G;
+  nz.rec = nz.slab_tot + (int64_t)g.G * g.S;
+  nz.rec_words = (int64_t)threads * bins;
+  return dispatch_dtype_nof64(dtype, [&](auto t) -> int {
+    using T = decltype(t);
+    if constexpr (sizeof(T) == 2) {
+      const size_t shr = ((size_t)kHistPatterns + (size_t)bins + (size_t)g.S * 16) * 4;
+      auto kern = hist_value_kernel<T, 2, kHvNz>;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+      }
+      count_dispatch(kDispHistValueNz);
+      kern<<<(unsigned)g.G, kHistValThreads, shr, stream>>>(reinterpret_cast<const T *>(x), nvec, g.vpb, hmax, bins,
+                                                           1, nullptr, HistChunks{}, nz);
+      if (threads > 1) {
+        const size_t shr_r = nz_recount_lds(g, bins);
+        static bool attr_r = false;
+        if (!attr_r) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void *>(hist_nz_recount_kernel<T>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          attr_r = true;
+        }
+        hist_nz_recount_kernel<T><<<dim3((unsigned)(threads - 1), (unsigned)g.S), kNzThreads, shr_r, stream>>>(
+            reinterpret_cast<const u32x4 *>(x), nvec, nz, g.G, threads, grain, hmax, bins);
+      }
+      constexpr int kFoldBW = 64;
+      const size_t shr_f = (size_t)(3 * g.G + 1 + 16) * 8 + (size_t)(16 + kNzFoldMaxRec) * kFoldBW * 4;
+      hist_nz_fold_kernel<kFoldBW><<<(unsigned)((bins + kFoldBW - 1) / kFoldBW), kFoldBW * 16, shr_f, stream>>>(
+          nz, g.G, threads, grain, bins, accum, accum_n, hist);
+      return check_launch();
+    }
+    return MTQ_ERR_DTYPE;
+  });
 }
 
 int64_t mtq_mse_workspace_floats(int64_t n, int dtype) {

@@ -1036,24 +1036,40 @@ at::Tensor histogram_abs_chunked(const at::Tensor &inputs, const at::Tensor &hma
   return hist;
 }
 
-// torch.histc's chunking with skip_zeros, all on the device: the non-zero chunk boundaries
-// (mtq_histogram_nonzero_bounds), then the one-launch chunked count over them
+// torch.histc's chunking with skip_zeros, all on the device and in one read of the input
+// (mtq_histogram_abs_nonzero_chunked)
 at::Tensor histogram_abs_chunked_nonzero(const at::Tensor &inputs, const at::Tensor &hmax, int64_t bins,
                                          int64_t threads, const c10::optional<at::Tensor> &scratch_in,
-                                         const c10::optional<at::Tensor> &accum) {
+                                         const c10::optional<at::Tensor> &accum_in) {
   at::Tensor x = inputs.contiguous();
   check_device(x, "inputs");
-  TORCH_CHECK(threads >= 1 && threads <= (1 << 20), "histogram_abs_chunked_nonzero: bad thread count");
+  TORCH_CHECK(hmax.scalar_type() == at::kFloat && hmax.numel() == 1, "histogram: hmax fp32 scalar");
+  TORCH_CHECK(threads >= 1 && threads <= 1024, "histogram_abs_chunked_nonzero: threads must be 1..1024");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  const int64_t ws = mtq_histogram_nonzero_bounds_workspace(x.numel());
-  TORCH_CHECK(ws >= 0, "histogram_abs_chunked_nonzero: bad size");
-  at::Tensor tiles = at::empty({ws > 0 ? ws : 1}, x.options().dtype(at::kInt));
-  at::Tensor bounds = at::empty({threads + 1}, x.options().dtype(at::kLong));
-  int st = mtq_histogram_nonzero_bounds(x.data_ptr(), x.numel(), checked_dtype(x, "inputs"), (int)threads,
-                                        32768, tiles.data_ptr<int32_t>(), ws, bounds.data_ptr<int64_t>(),
-                                        cur_stream(x));
-  check_status(st, "histogram_nonzero_bounds");
-  return histogram_abs_chunked(x, hmax, bins, true, bounds, 0, threads, scratch_in, accum);
+  const int64_t words = mtq_histogram_nonzero_scratch_words(x.numel(), (int)threads, (int)bins);
+  TORCH_CHECK(words >= 0, "histogram_abs_chunked_nonzero: bad size (bins <= 8176)");
+  at::Tensor scratch;
+  if (scratch_in.has_value() && scratch_in->defined()) {
+    scratch = *scratch_in;
+    TORCH_CHECK(scratch.scalar_type() == at::kInt && scratch.is_contiguous() && scratch.device() == x.device(),
+                "histogram_abs_chunked_nonzero: scratch must be contiguous int32 on the input's device");
+  }
+  if (!scratch.defined() || scratch.numel() < words) scratch = at::empty({words > 0 ? words : 1}, x.options().dtype(at::kInt));
+  at::Tensor accum;
+  if (accum_in.has_value() && accum_in->defined()) {
+    accum = accum_in->contiguous();
+    TORCH_CHECK(accum.scalar_type() == at::kFloat && accum.dim() == 1 && accum.numel() <= bins &&
+                    accum.device() == x.device(),
+                "histogram_abs_chunked_nonzero: accum must be fp32 [<= bins] on the input's device");
+  }
+  at::Tensor hist = at::empty({bins}, x.options().dtype(at::kFloat));
+  int st = mtq_histogram_abs_nonzero_chunked(
+      x.data_ptr(), x.numel(), checked_dtype(x, "inputs"), hmax.data_ptr<float>(), (int)bins, (int)threads, 32768,
+      reinterpret_cast<uint32_t *>(scratch.data_ptr<int32_t>()), scratch.numel(),
+      accum.defined() ? accum.data_ptr<float>() : nullptr, accum.defined() ? accum.numel() : 0,
+      hist.data_ptr<float>(), cur_stream(x));
+  check_status(st, "histogram_abs_chunked_nonzero");
+  return hist;
 }
 
 // ---- reference torch.library ops (tensor_quant.py:115-195) -------------------------------------

@@ -148,6 +148,11 @@ def _histc_threads() -> int:
     return max(1, int(env)) if env else max(1, torch.get_num_threads())
 
 
+# the one-read skip_zeros path (csrc/mtq_kernels.hip mtq_histogram_abs_nonzero_chunked) takes up to
+# ~6e10 elements; larger calls take the per-chunk path
+_NZ_ONE_READ_MAX_ELEMS = 50_000_000_000
+
+
 def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bool,
                   threads: int | None = None, accum: torch.Tensor | None = None) -> torch.Tensor:
     """fp32 per-call histogram of |x| over [0, hmax] with torch.histc's CPU accumulation.
@@ -178,11 +183,11 @@ def _histc_counts(x: torch.Tensor, hmax: torch.Tensor, bins: int, skip_zeros: bo
     flat = x.contiguous().reshape(-1)
     gpu_one_launch = (flat.is_cuda and flat.dtype in (torch.bfloat16, torch.float16) and bins <= 8192
                       and n % 8 == 0 and flat.data_ptr() % 16 == 0)
-    if skip_zeros and gpu_one_launch:
-        # the non-zero chunk boundaries found on the device (per-tile non-zero counts, then one
-        # block per boundary), no host sync; with at most 2^24 non-zeros every count is exact in
-        # fp32, so the chunked sum equals the single-launch count there too
-        t = threads or _histc_threads()
+    t = threads or _histc_threads()
+    if skip_zeros and gpu_one_launch and bins <= 8176 and t <= 1024 and n <= _NZ_ONE_READ_MAX_ELEMS:
+        # the non-zero chunks counted on the device in one read of the input, no host sync (the
+        # boundaries resolved afterwards from per-slab non-zero counts); with at most 2^24
+        # non-zeros every count is exact in fp32, so the chunked sum equals the single-launch count
         return ops.histogram_abs_chunked_nonzero(flat, hmax, bins, t, None, accum)
     if skip_zeros:
         # chunk boundaries live in the compacted (non-zero) index space: map them back

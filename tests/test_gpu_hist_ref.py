@@ -265,3 +265,20 @@ def test_histc_skip_zeros_above_2p24_no_host_sync(gpu):
     exact = torch.zeros(2048, dtype=torch.int32, device=gpu)
     ops.histogram_abs_accumulate(x, hmax, exact, 2048, True)
     assert torch.equal(got, exact.float())  # 0.75 n non-zeros < 2^24: every count exact
+
+
+def test_histc_chunked_empty_input_reads_nothing(gpu):
+    """an empty call of the chunked / non-zero-chunked ops (C ABI reachable) returns the
+    running histogram (or zeros) without launching a count over the input."""
+    from modelopt_amd import _ext
+
+    ops = _ext.ops()
+    hmax = torch.tensor([4.0], device=gpu)
+    empty = torch.empty(0, dtype=torch.bfloat16, device=gpu)
+    acc = torch.arange(100, dtype=torch.float32, device=gpu)
+    for accum, want in ((None, torch.zeros(2048)), (acc, torch.cat([acc.cpu(), torch.zeros(1948)]))):
+        got = ops.histogram_abs_chunked_nonzero(empty, hmax, 2048, 16, None, accum)
+        assert torch.equal(got.cpu(), want)
+        bounds = torch.zeros(17, dtype=torch.int64, device=gpu)
+        got = ops.histogram_abs_chunked(empty, hmax, 2048, True, bounds, 0, 16, None, accum)
+        assert torch.equal(got.cpu(), want)
