@@ -1954,11 +1954,13 @@ __global__ __launch_bounds__(BW * 16) void hist_nz_fold_kernel(HistNz nz, int G,
   uint32_t *recl = acc + 16 * BW;                               // [kNzFoldMaxRec][BW]
   const int bl = threadIdx.x % BW, gl = threadIdx.x / BW, bn = blockIdx.x * BW + bl;
   const int bnc = bn < bins ? bn : bins - 1;
-  // this lane's rows (G <= 256 in one batch of 16 loads; more in further batches below)
+  // this lane's rows: ranges 16 gl .. 16 gl + 15 (consecutive, so mostly one chunk: summed in a
+  // register and added to LDS once per chunk change); G <= 256 in one batch of 16 loads
+  const int wl = G <= 256 ? 16 : (G + 15) / 16;  // ranges per lane
   uint32_t v[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int w = gl + 16 * k < G ? gl + 16 * k : G - 1;
+    const int w = gl * wl + k < G ? gl * wl + k : G - 1;
     v[k] = nz.rows[(int64_t)w * bins + bnc];
   }
   // the first group's boundary rows (rec[1 .. 16]) and the range totals, loaded beside the rows:
@@ -1991,38 +1993,44 @@ __global__ __launch_bounds__(BW * 16) void hist_nz_fold_kernel(HistNz nz, int G,
     // boundary rows g0 + 1 .. g1 (rec[c + 1] for the group's chunks), staged in LDS slot (c - g0)
     if (g0 > 0 && g0 + gl + 1 < ck.teff) recl[gl * BW + bl] = nz.rec[(g0 + gl + 1) * bins + bnc];
     __syncthreads();
-    for (int w0 = 0; w0 < G; w0 += 256) {
+    int64_t run_c = -1;
+    uint32_t run = 0;
+    for (int k0 = 0; k0 < wl; k0 += 16) {
       uint32_t vv[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        if (w0 == 0) {
+        if (k0 == 0) {
           vv[k] = v[k];
         } else {
-          const int w = w0 + gl + 16 * k < G ? w0 + gl + 16 * k : G - 1;
-          vv[k] = nz.rows[(int64_t)w * bins + bnc];
+          const int w = gl * wl + k0 + k;
+          vv[k] = nz.rows[(int64_t)(w < G ? w : G - 1) * bins + bnc];
         }
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int w = w0 + gl + 16 * k;
-        if (w >= G) break;
+        const int w = gl * wl + k0 + k;
+        if (k0 + k >= wl || w >= G) break;
         const int64_t cf = cfl[2 * w], cl = cfl[2 * w + 1];  // first / last chunk of its ranks
         if (cf < 0 || cl < g0 || cf >= g1) continue;  // no non-zeros (an all-zero row), or another group
         if (cf == cl) {
-          atomicAdd(acc + (cf - g0) * BW + bl, vv[k]);
+          if (cf != run_c) {
+            if (run_c >= 0) atomicAdd(acc + (run_c - g0) * BW + bl, run);
+            run_c = cf;
+            run = 0;
+          }
+          run += vv[k];
           continue;
         }
         uint32_t rest = vv[k];
         for (int64_t c = cf; c < cl; ++c) {  // the segment before boundary c + 1 goes to chunk c
-          const int64_t j = c + 1 - g0 - 1;  // slot of rec[c + 1] when staged (c in the group)
-          const uint32_t r = (c >= g0 && c < g1 && c + 1 <= g0 + 16) ? recl[j * BW + bl]
-                                                                    : nz.rec[(c + 1) * bins + bnc];
+          const uint32_t r = (c >= g0 && c < g1) ? recl[(c - g0) * BW + bl] : nz.rec[(c + 1) * bins + bnc];
           rest -= r;
           if (c >= g0 && c < g1) atomicAdd(acc + (c - g0) * BW + bl, r);
         }
         if (cl < g1) atomicAdd(acc + (cl - g0) * BW + bl, rest);
       }
     }
+    if (run_c >= 0) atomicAdd(acc + (run_c - g0) * BW + bl, run);
     __syncthreads();
     if (gl == 0 && bn < bins)
       for (int64_t c = g0; c < g1; ++c) h += fminf((float)acc[(c - g0) * BW + bl], 16777216.f);
