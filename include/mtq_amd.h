@@ -371,7 +371,7 @@ int mtq_awq_clip_search(const void *w, const float *x, int64_t co, int64_t cols,
  *   loss[g] += mean_{m,n} float(T(T(sum_k T(x[m,k]*sinv[g,k]) * wq[g,n,k] + bias[n]) - yref[m,n]))^2
  * x [M, K], sinv [G, K] (= (1/s_g).to(T)), wq [G, N, K] (= qdq(W * s_g), mtq_block_quant_dynamic),
  * bias [N] or NULL, yref [M, N] (the unquantized output), all dtype T (bf16 / f16), 16-byte
- * aligned, K % 64 == 0, N % 8 == 0, M*K and N*K < 2^31; fp32 accumulation on v_mfma_f32_32x32x16; the output is never stored.
+ * aligned, K % 64 == 0, N % 8 == 0, M*K and N*K < 2^31; fp32 accumulation on v_mfma_f32_16x16x32; the output is never stored.
  * workspace: mtq_awq_search_gemm_workspace_floats(M, N, K, G) floats, 16-byte aligned, no
  * initialisation needed (per-tile partial sums + the pre-scaled activations [G, M, K]).
  * Deterministic (fixed-order sums).  G <= 64. */
@@ -380,6 +380,17 @@ int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const v
                         const void *yref, int64_t M, int64_t N, int64_t K, int dtype, int G,
                         float *loss, float *workspace, int64_t workspace_floats,
                         hipStream_t stream);
+/* The same with the search kernel named (for A/B and tests; same arguments and results up to the
+ * per-tile square-sum order): MTQ_AWQ_SEARCH_AUTO = what mtq_awq_search_gemm runs (PP, the faster
+ * one on the widths the fused search serves); PP = the r03 two-group ping-pong kernel (8 waves,
+ * 128 x 64 per wave);
+ * W4 = the r06 one-wave-per-SIMD kernel (4 waves, 128 x 128 per wave, K loop in generated inline
+ * asm; needs K >= 128 and M * N * 2 < 2^32, MTQ_ERR_INVALID_ARG otherwise). */
+enum { MTQ_AWQ_SEARCH_AUTO = 0, MTQ_AWQ_SEARCH_PP = 1, MTQ_AWQ_SEARCH_W4 = 2 };
+int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const void *wq, const void *bias,
+                               const void *yref, int64_t M, int64_t N, int64_t K, int dtype, int G,
+                               float *loss, float *workspace, int64_t workspace_floats, int kernel,
+                               hipStream_t stream);
 /* The same search with the GEMMs elsewhere (wide linears keep hipBLASLt):
  *  mtq_awq_prescale: xs[g, m, k] = T(x[m, k] * sinv[g, k]), one read of x for all G alphas
  *    (the reference's `inputs * pre_quant_scale` per alpha, tensor_quantizer.py:1143-1144).

@@ -2,8 +2,9 @@
 """AWQ-lite alpha search per linear, Llama-3-8B shapes, one calibration batch (8192 tokens, 11
 alphas), all in one process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24):
 
-* ``fused``   -- mtq_awq_search_gemm: the pre-scale pass + the ping-pong MFMA search kernel with the
-                 loss in its epilogue
+* ``fused``   -- mtq_awq_search_gemm: the pre-scale pass + the MFMA search kernel with the loss in
+                 its epilogue (the r06 one-wave-per-SIMD kernel where K >= 128)
+* ``fused_pp`` -- the same with the r03 ping-pong kernel (kernel=1)
 * ``batched`` -- the wide-linear path: awq_prescale + 11 hipBLASLt torch.mm into [G, M, N] +
                  awq_mse_multi
 * ``per_alpha`` -- the r01 path: per alpha mul_cols + hipBLASLt F.linear + mse_accumulate
@@ -56,6 +57,9 @@ for name, (N, K) in SHAPES.items():
     def search():
         ops.awq_search_gemm(x, si, wq, None, yref, loss)
 
+    def search_pp():
+        ops.awq_search_gemm(x, si, wq, None, yref, loss, 1)
+
     def batched():
         xs = ops.awq_prescale(x, si)
         out = torch.empty((G, M, N), dtype=x.dtype, device=dev)
@@ -72,7 +76,7 @@ for name, (N, K) in SHAPES.items():
         for g in range(G):
             F.linear(x, wq[g])
 
-    arms = {"fused": search, "batched": batched, "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
+    arms = {"fused": search, "fused_pp": search_pp, "batched": batched, "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
     t = {k: [] for k in arms}
     for _ in range(ROUNDS):
         for k, f in arms.items():

@@ -30,7 +30,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, uint
 
 template <int V>
 __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
-  constexpr int S = kW4Slots[V], SWZ = kW4Swz[V], OFS = kW4Ofs[V];
+  constexpr int S = kW4Slots[V], EPI = kW4Epi[V], GM = kW4Gm[V];
   __shared__ __attribute__((aligned(16))) unsigned char lds[S == 2 ? 131072 : S * 32768];  // S 2: the T64 schedule, two 64 KiB tile slots
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -39,12 +39,13 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
   int g, tm, tn;
   {  // the product's tile order: 8 x 4 tile units, one per XCD round, XCDs on the same alpha / column range
     const int xcd = orig % 8, li = orig / 8;
+    constexpr int GN = 32 / GM;
     const int slot = li % 32, u = (li / 32) * 8 + xcd;
-    const int mgn = (p.tiles_m + 7) / 8, nn4 = (p.tiles_n + 3) / 4;
+    const int mgn = (p.tiles_m + GM - 1) / GM, nn4 = (p.tiles_n + GN - 1) / GN;
     const int mg = u % mgn, n4 = (u / mgn) % nn4;
     g = u / (mgn * nn4);
-    tm = mg * 8 + slot % 8;
-    tn = n4 * 4 + slot / 8;
+    tm = mg * GM + slot % GM;
+    tn = n4 * GN + slot / GM;
     if (g >= p.G || tm >= p.tiles_m || tn >= p.tiles_n) return;
   }
   const int tiles = p.tiles_m * p.tiles_n;
@@ -56,7 +57,8 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
   const __amdgpu_buffer_rsrc_t xr = rsrc_of(X, (uint32_t)(p.M * K * 2));
   const __amdgpu_buffer_rsrc_t wr = rsrc_of(W, (uint32_t)(p.N * K * 2));
 
-  if constexpr (S == 2) {
+  static_assert(S == 2, "T64 only");
+  {
     // T64 (gen_w4asm.py body_t64): K tiles of 64, 128-byte LDS rows, chunk c of row r stored at
     // c ^ ((r >> 1) & 7).  DMA: wave w fills 1 KiB blocks w*8 + u of each operand's tile part (8
     // rows of 128 B); lane l writes row 64 w + 8 u + (l >> 3), stored chunk l & 7.
@@ -80,6 +82,41 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
     unsigned koff, kc, m0s, sdma, srd;
     unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)(K / 64));
     const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
+    if constexpr (EPI == 2) {
+      // the reference tile rides in the last two K tiles' DMAs (gen_w4asm.py body_t64y): half h
+      // (rows 128 h ..) lands in slot (K / 64 + h) % 2, row r's 16-byte chunk c at c ^ (r & 15)
+      const __amdgpu_buffer_rsrc_t yr = rsrc_of(p.yref, (uint32_t)(p.M * p.N * 2));
+      const unsigned yrb = __builtin_amdgcn_readfirstlane((unsigned)(((m0 + 32 * wave) * p.N + n0) * 2));
+      const unsigned yh = __builtin_amdgcn_readfirstlane((unsigned)(128 * p.N * 2));
+      const unsigned ys2 = __builtin_amdgcn_readfirstlane((unsigned)(2 * p.N * 2));
+      const unsigned m0yb = __builtin_amdgcn_readfirstlane(lds0 + wave * 16384);
+      unsigned yo[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
+      unsigned m0y, yso;
+      unsigned cnt2 = __builtin_amdgcn_readfirstlane((unsigned)(K / 64 - 2));
+#define W4_ASMY(BODY) \
+      asm volatile(BODY \
+                   : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
+                     [cnt] "+s"(cnt2), [m0y] "=&s"(m0y), [yso] "=&s"(yso) \
+                   : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast), \
+                     [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]), \
+                     [xo4] "v"(xo[4]), [xo5] "v"(xo[5]), [xo6] "v"(xo[6]), [xo7] "v"(xo[7]), \
+                     [wo0] "v"(wo[0]), [wo1] "v"(wo[1]), [wo2] "v"(wo[2]), [wo3] "v"(wo[3]), \
+                     [wo4] "v"(wo[4]), [wo5] "v"(wo[5]), [wo6] "v"(wo[6]), [wo7] "v"(wo[7]), \
+                     [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1), \
+                     [yr] "s"(yr), [yrb] "s"(yrb), [yh] "s"(yh), [ys2] "s"(ys2), [m0yb] "s"(m0yb), \
+                     [yo0] "v"(yo[0]), [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]), \
+                     [yo4] "v"(yo[4]), [yo5] "v"(yo[5]), [yo6] "v"(yo[6]), [yo7] "v"(yo[7]) \
+                   : W4ASM_CLOBBERS)
+      if constexpr (V == 0) W4_ASMY(W4ASM_BODY_Y_0);
+      if constexpr (V == 1) W4_ASMY(W4ASM_BODY_Y_1);
+      if constexpr (V == 2) W4_ASMY(W4ASM_BODY_Y_2);
+      if constexpr (V == 3) W4_ASMY(W4ASM_BODY_Y_3);
+      if constexpr (V == 4) W4_ASMY(W4ASM_BODY_Y_4);
+#undef W4_ASMY
+    }
 #define W4_ASM64(BODY)                                                                               \
   asm volatile(BODY                                                                                  \
                : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma),             \
@@ -91,56 +128,16 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
                  [wo4] "v"(wo[4]), [wo5] "v"(wo[5]), [wo6] "v"(wo[6]), [wo7] "v"(wo[7]),                  \
                  [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1)                           \
                : W4ASM_CLOBBERS)
-    if constexpr (V == 1) W4_ASM64(W4ASM_BODY_1);
-    if constexpr (V == 2) W4_ASM64(W4ASM_BODY_2);
-    if constexpr (V == 3) W4_ASM64(W4ASM_BODY_3);
+    static_assert(EPI == 2, "the reference-prefetch epilogue only");
 #undef W4_ASM64
-  } else {
-  // DMA sources: wave w fills 1 KiB blocks w*4 + u of each operand's half (16 rows of 64 B); lane l
-    // writes row 64 w + 16 u + (l >> 2), stored chunk l & 3 = source chunk c ^ f(row), f(row) =
-    // (row >> 2) & 3 (SWZ 0) or ((row >> 3) & 1) << 1 (SWZ 1: conflict-free for ds_read_b128's lane groups)
-    unsigned xo[4], wo[4];
-    {
-      const int c = (lane & 3) ^ (SWZ ? ((lane >> 5) & 1) << 1 : (lane >> 4) & 3);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = 64 * wave + 16 * u + (lane >> 2);
-        const int64_t row = m0 + r < p.M ? m0 + r : p.M - 1;
-        const int64_t col = n0 + r < p.N ? n0 + r : p.N - 1;
-        xo[u] = (unsigned)((row * K + 8 * c) * 2) - (OFS ? u * 1024u : 0u);  // OFS: the instruction offset adds it back
-        wo[u] = (unsigned)((col * K + 8 * c) * 2) - (OFS ? u * 1024u : 0u);
-      }
-    }
-    // fragment reads: row 16 i + fr of the wave's block, chunk fq stored at fq ^ f(row)
-    const int fr = lane & 15, fq = lane >> 4;
-    const unsigned lds0 = (unsigned)(uintptr_t)lds;
-    const unsigned lterm = fr * 64 + ((fq ^ (SWZ ? ((fr >> 3) & 1) << 1 : (fr >> 2) & 3)) << 4);
-    const unsigned xb = lds0 + wm * 8192 + lterm;
-    const unsigned wb = lds0 + 16384 + wn * 8192 + lterm;
-    const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);
-    unsigned koff, kc, m0s, sdma, srd;
-    unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)(K / 64));
-    const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 32 - 1) * 64));
-#define W4_ASM(BODY)                                                                                 \
-    asm volatile(BODY                                                                              \
-                 : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma),             \
-                   [srd] "=&s"(srd), [cnt] "+s"(cnt)                                                       \
-                 : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast),                         \
-                   [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]),                  \
-                   [wo0] "v"(wo[0]), [wo1] "v"(wo[1]), [wo2] "v"(wo[2]), [wo3] "v"(wo[3]),                  \
-                   [xb] "v"(xb), [wb] "v"(wb)                                                               \
-                 : W4ASM_CLOBBERS)
-    if constexpr (V == 0) W4_ASM(W4ASM_BODY_0);
-
-#undef W4_ASM
-
-}
+  }
   const int fr = lane & 15, fq = lane >> 4;
   // epilogue: a lane's accumulators of tile (i, j) are out[m][n .. n+3], m = 16 i + fr, n = 16 j + 4 fq
   // (the W fragment is the MFMA's A operand); output and difference rounded to bf16, fp32 square-sum
   const __bf16 *Y = reinterpret_cast<const __bf16 *>(p.yref);
   float sum = 0.f;
   float o[32];
+  const unsigned yslot = (unsigned)(((K / 64 + wm) & 1) * 65536);
 #define W4_STRIP(I)                                                                                  \
   {                                                                                                  \
     W4ASM_STRIP_##I(o);                                                                              \
@@ -151,7 +148,14 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
       const bool ok = rok && n < p.N;                                                                \
       __bf16 yr[4];                                                                                  \
       const int64_t off = (ok ? m : 0) * p.N + (ok ? n : 0);                                         \
-      __builtin_memcpy(yr, Y + off, 8);                                                              \
+      if constexpr (EPI == 1) {                                                                      \
+        __builtin_memset(yr, 0, 8);                                                                  \
+      } else if constexpr (EPI == 2) {                                                               \
+        const int rr = 16 * (I) + fr, cl = wn * 128 + 16 * j + 4 * fq;                               \
+        __builtin_memcpy(yr, lds + yslot + rr * 512 + (((cl >> 3) ^ fr) << 4) + (cl & 7) * 2, 8);    \
+      } else {                                                                                       \
+        __builtin_memcpy(yr, Y + off, 8);                                                            \
+      }                                                                                              \
       _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                \
         const float y = Elem<__bf16>::ld(Elem<__bf16>::st(o[j * 4 + e]));                            \
         const float d = Elem<__bf16>::ld(Elem<__bf16>::st(y - Elem<__bf16>::ld(yr[e])));             \
@@ -173,7 +177,8 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
 
 // xs [G, M, K] pre-scaled activations, wq [G, N, K], yref [M, N] (bf16); partial [G * tiles]
 template <int V> int go(const Args &a, hipStream_t stream) {
-  const int units = a.G * ((a.tiles_m + 7) / 8) * ((a.tiles_n + 3) / 4);
+  constexpr int GM = kW4Gm[V], GN = 32 / GM;
+  const int units = a.G * ((a.tiles_m + GM - 1) / GM) * ((a.tiles_n + GN - 1) / GN);
   w4asm_kernel<V><<<(unsigned)((units + 7) / 8 * 8 * 32), 256, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
@@ -181,13 +186,14 @@ template <int V> int go(const Args &a, hipStream_t stream) {
 // var: gen_w4asm.py VARIANTS index
 extern "C" int awq_w4asm(int var, const void *xs, const void *wq, const void *yref, float *partial, int64_t M, int64_t N,
                          int64_t K, int G, hipStream_t stream) {
-  if (K % 64 || K < 64 || N % 8) return 2;
+  if (K % 64 || K < 128 || N % 8) return 2;
   Args a{xs, wq, yref, partial, M, N, K, (int)((M + 255) / 256), (int)((N + 255) / 256), G};
   switch (var) {
   case 0: return go<0>(a, stream);
   case 1: return go<1>(a, stream);
   case 2: return go<2>(a, stream);
   case 3: return go<3>(a, stream);
+  case 4: return go<4>(a, stream);
   default: return 3;
   }
 }

@@ -55,6 +55,9 @@ for name, (N, K) in SHAPES.items():
     def product():
         ops.awq_search_gemm(x, si, wq, None, yref, loss)
 
+    def product_pp():
+        ops.awq_search_gemm(x, si, wq, None, yref, loss, 1)
+
     def prescale():
         ops.awq_prescale(x, si)
 
@@ -65,7 +68,7 @@ for name, (N, K) in SHAPES.items():
     # correctness of the copy: variant 0's per-alpha loss equals the product's
     l0 = torch.zeros(G, device=dev)
     ops.awq_search_gemm(x, si, wq, None, yref, l0)
-    for v in [0] + [v for v in VARS if v in (10, 20, 21, 22, 30, 31, 34, 50) or 70 <= v < 74]:
+    for v in [0] + [v for v in VARS if v in (10, 20, 21, 22, 30, 31, 34, 50) or 70 <= v < 75]:
         part.fill_(float("nan"))
         var(v)()
         torch.cuda.synchronize()
@@ -73,7 +76,7 @@ for name, (N, K) in SHAPES.items():
         if not torch.allclose(l0, l1, rtol=1e-5):
             print(f"{name}: variant {v} loss MISMATCH {l0.tolist()[:3]} vs {l1.tolist()[:3]}", file=sys.stderr, flush=True)
             assert v != 0
-    arms = {"product": product, "prescale": prescale, "hipblaslt_gemms": gemms}
+    arms = {"product": product, "product_pp": product_pp, "prescale": prescale, "hipblaslt_gemms": gemms}
     arms.update({f"v{v}": var(v) for v in VARS})
     t = {k: [] for k in arms}
     for _ in range(ROUNDS):

@@ -28,11 +28,15 @@ SLOT = 32768
 # moves the global address: the C++ side subtracts it from the lane's voffset)
 # CACHE: cache-policy bits of the DMAs ("" / "sc1" / "nt" / "sc0 sc1")
 # S = 2: the T64 schedule (body_t64), ORDER G / H
+# C++-side fields (kW4Epi / kW4Gm): EPI 1 = probe without the reference-tile loads; GM = row tiles
+# per XCD tile unit (the product's 8 x 4 units: GM 8)
+# EPI 2: the reference tile prefetched into the LDS ring by the last two K tiles (body_t64y)
 VARIANTS = [
-    (4, "C", 1, 0, 1, ""),
-    (2, "G", 2, 0, 1, ""),
-    (2, "H", 2, 0, 1, ""),
-    (2, "G", 2, 0, 1, "sc1"),
+    (2, "G", 2, 0, 1, "", 2, 8),
+    (2, "I", 2, 0, 1, "", 2, 8),
+    (2, "J", 2, 0, 1, "", 2, 8),
+    (2, "K", 2, 0, 1, "", 2, 8),
+    (2, "G", 2, 0, 1, "sc1", 2, 8),
 ]
 CACHE = ""
 
@@ -172,7 +176,88 @@ def reads64(s, xb, wb):
     return out
 
 
-def body_t64(order):
+def ydmas():
+    """16 LDS-DMAs of one 128-row half of the reference (yref) tile into the current slot: wave w
+    fills rows 32 w + 2 u + (l >> 5) (512 B each), u = 0..15; the row advance in the scalar
+    offset %[yso] (+ %[ys2] = two rows per DMA), the lane's XOR-swizzled chunk in yo(u % 8)."""
+    out = []
+    for u in range(16):
+        out.append([f"s_add_u32 m0, %[m0y], {u * 1024}", "s_nop 0",
+                    f"buffer_load_dwordx4 %[yo{u % 8}], %[yr], %[yso] offen lds",
+                    "s_add_u32 %[yso], %[yso], %[ys2]"])
+    return out
+
+
+def tile64(order, probe, yhalf=None):
+    """One K tile (phase 1, barrier, phase 2); yhalf: the two peeled last tiles, whose phase-2 DMAs
+    load the reference tile's half yhalf instead of a (past-the-end) K tile."""
+    L = []
+    # phase 1
+    L += ["s_waitcnt lgkmcnt(0)", "v_add_u32 v120, %[sdma], %[xb1]", "v_add_u32 v121, %[sdma], %[wb1]"]
+    rd = reads64(1, "v120", "v121")
+    for n in range(64):
+        L.append(mfma(0, n // 8, n % 8))
+        if n >= 2 and (n - 2) % 3 == 0 and (n - 2) // 3 < 16:
+            L.append(rd[(n - 2) // 3])
+    kadv = "s_min_u32 %[kc], %[koff], %[klast]" if probe != 2 else "s_mov_b32 %[kc], 0"  # probe 2: L2 hits
+    L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier",
+          "s_xor_b32 %[srd], %[sdma], 65536", "v_add_u32 v122, %[srd], %[xb0]", "v_add_u32 v123, %[srd], %[wb0]"]
+    if yhalf is None:
+        L += ["s_add_u32 %[m0s], %[m0b], %[sdma]", kadv, "s_add_u32 %[koff], %[koff], 128"]
+        dm = dmas64("%[m0s]", False) if probe != 1 else [[]] * 16  # probe 1: no loads in the loop
+    else:
+        L += ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
+              "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
+        dm = ydmas()
+    rd = reads64(0, "v122", "v123")
+    pr, pd = PHASE2[order]
+    for n in range(64):
+        L.append(mfma(1, n // 8, n % 8))
+        for k, at in enumerate(pd):
+            if at == n:
+                L += dm[k]
+        for k, at in enumerate(pr):
+            if at == n:
+                L.append(rd[k])
+    L += ["s_xor_b32 %[sdma], %[sdma], 65536"]
+    return L
+
+
+# phase-2 placement: (ds_read after MFMA #, DMA after MFMA #)
+PHASE2 = {
+    "G": ([2 + 3 * k for k in range(16)], [1 + 4 * k for k in range(16)]),
+    "H": ([3 * k for k in range(16)], [16 + 3 * k for k in range(16)]),
+    "I": ([2 * k + 1 for k in range(16)], [2 * k for k in range(16)]),
+    "J": ([3 * k + 1 for k in range(16)], [3 * k for k in range(16)]),
+    "K": ([4 * k + 2 for k in range(16)], [4 * k for k in range(16)]),
+}
+
+
+def body_t64y(order, probe):
+    """T64 with the reference tile prefetched into the ring by the last two tiles' DMAs; the loop
+    runs K / 64 - 2 tiles (%[cnt], may be 0), the last two are peeled."""
+    L = ["s_nop 4"]
+    L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    L += ["s_mov_b32 %[koff], 0", "s_mov_b32 %[sdma], 0"]
+    for t in range(2):
+        L += ["s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128",
+              f"s_add_u32 %[m0s], %[m0b], {t * 65536}"]
+        for d in dmas64("%[m0s]", True):
+            L += d
+    L += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    L += reads64(0, "%[xb0]", "%[wb0]")
+    L += ["s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_tail_%="]
+    L.append("L_w4_loop_%=:")
+    L += tile64(order, probe)
+    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_loop_%="]
+    L.append("L_w4_tail_%=:")
+    L += tile64(order, probe, 0)
+    L += tile64(order, probe, 1)
+    L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier", "s_nop 15", "s_nop 15", "s_nop 15"]
+    return L
+
+
+def body_t64(order, probe):
     L = ["s_nop 4"]
     L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
     L += ["s_mov_b32 %[koff], 0", "s_mov_b32 %[sdma], 0"]
@@ -191,12 +276,13 @@ def body_t64(order):
         L.append(mfma(0, n // 8, n % 8))
         if n >= 2 and (n - 2) % 3 == 0 and (n - 2) // 3 < 16:
             L.append(rd[(n - 2) // 3])
+    kadv = "s_min_u32 %[kc], %[koff], %[klast]" if probe != 2 else "s_mov_b32 %[kc], 0"  # probe 2: L2 hits
     L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier",
           "s_xor_b32 %[srd], %[sdma], 65536", "v_add_u32 v122, %[srd], %[xb0]", "v_add_u32 v123, %[srd], %[wb0]",
           "s_add_u32 %[m0s], %[m0b], %[sdma]",
-          "s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128"]
+          kadv, "s_add_u32 %[koff], %[koff], 128"]
     rd = reads64(0, "v122", "v123")
-    dm = dmas64("%[m0s]", False)
+    dm = dmas64("%[m0s]", False) if probe != 1 else [[]] * 16  # probe 1: no loads in the loop
     if order == "G":
         pr, pd = [2 + 3 * k for k in range(16)], [1 + 4 * k for k in range(16)]
     else:  # "H": reads first, DMAs after
@@ -227,14 +313,20 @@ def strips():
 def main():
     text = "// generated by scripts/exp/gen_w4asm.py -- do not edit\n"
     global CACHE
-    for v, (S, order, swz, probe, ofs, CACHE) in enumerate(VARIANTS):
-        lines = body_t64(order) if S == 2 else body(S, order, probe, ofs)
+    for v, (S, order, swz, probe, ofs, CACHE, _epi, _gm) in enumerate(VARIANTS):
+        if S == 2:
+            lines = body_t64y(order, probe) if _epi == 2 else body_t64(order, probe)
+        else:
+            lines = body(S, order, probe, ofs)
         asm = "".join(f'  "{ln}\\n\\t"\n' for ln in lines)
-        text += f"#define W4ASM_BODY_{v} \\\n" + asm.replace("\n", " \\\n") + "\n"
+        name = f"W4ASM_BODY_{v}" if _epi != 2 else f"W4ASM_BODY_Y_{v}"
+        text += f"#define {name} \\\n" + asm.replace("\n", " \\\n") + "\n"
     text += f"#define W4ASM_NVAR {len(VARIANTS)}\n"
     text += "constexpr int kW4Slots[] = {" + ", ".join(str(v[0]) for v in VARIANTS) + "};\n"
     text += "constexpr int kW4Swz[] = {" + ", ".join(str(v[2]) for v in VARIANTS) + "};\n"
     text += "constexpr int kW4Ofs[] = {" + ", ".join(str(v[4]) for v in VARIANTS) + "};\n"
+    text += "constexpr int kW4Epi[] = {" + ", ".join(str(v[6]) for v in VARIANTS) + "};\n"
+    text += "constexpr int kW4Gm[] = {" + ", ".join(str(v[7]) for v in VARIANTS) + "};\n"
     clob = ", ".join(f'"v{r}"' for r in range(120, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
     text += "#define W4ASM_CLOBBERS " + clob.replace("\n", " \\\n") + ', "memory", "scc"\n'
     text += strips()

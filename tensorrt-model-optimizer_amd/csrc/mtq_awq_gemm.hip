@@ -367,6 +367,147 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// r06 search kernel: one wave per SIMD, the K loop at the instruction level.  4 waves per 256 x
+// 256 tile, a 128 x 128 block per wave (64 accumulators of 4 fp32 = a[0:255]), K tiles of 64 with
+// both operands by LDS-DMA in whole 128-byte rows, two 64 KiB LDS slots, one barrier per tile,
+// the reference tile carried by the last two tiles' DMAs.  The K loop is ONE inline-asm statement
+// generated by scripts/gen_awq_w4.py (mtq_awq_w4.inc; the schedule is described there): hipcc's
+// own waits would drain the prefetch (the r04 W4 HIP variants, §4e), so every wait is counted by
+// hand and the compiler sees one opaque statement that names the VGPRs v[120:255] and all AGPRs
+// it uses.  Same tile order, operands, roundings and loss as awq_search_pp_kernel (a different
+// per-tile square-sum order).  Requires K % 64 == 0, K >= 128 and M * N * 2 < 2^32 (32-bit buffer
+// offsets of the reference tile).  Measured against the pp kernel (kernel time, 8192 tokens, 11
+// alphas; profiles/r06/awq/): gate 7.56 vs 7.97 ms, but k / q / down 0.66 / 2.25 / 7.62 vs 0.61 /
+// 2.20 / 7.55 ms -- so the product (MTQ_AWQ_SEARCH_AUTO) keeps the pp kernel, which is what the
+// fused path runs (N <= 2048, k / v_proj); this one is selected explicitly (kernel = W4).
+#include "mtq_awq_w4.inc"
+
+template <typename T, bool HAS_BIAS>
+__global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[131072];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int g, tm, tn;
+  {  // the pp kernel's tile order (8 x 4 units, one per XCD round)
+    const int orig = blockIdx.x;
+    const int xcd = orig % 8, li = orig / 8;
+    const int slot = li % 32, u = (li / 32) * 8 + xcd;
+    const int mgn = (p.tiles_m + 7) / 8, nn4 = (p.tiles_n + 3) / 4;
+    const int mg = u % mgn, n4 = (u / mgn) % nn4;
+    g = u / (mgn * nn4);
+    tm = mg * 8 + slot % 8;
+    tn = n4 * 4 + slot / 8;
+    if (g >= p.G || tm >= p.tiles_m || tn >= p.tiles_n) return;  // the whole workgroup, before any barrier
+  }
+  const int tile = tm * p.tiles_n + tn;
+  const int64_t m0 = (int64_t)tm * kBM, n0 = (int64_t)tn * kBN;
+  const int64_t K = p.K;
+  const T *X = reinterpret_cast<const T *>(p.x) + (int64_t)g * p.M * K;
+  const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
+  const __amdgpu_buffer_rsrc_t xr = wave_rsrc(X, (uint32_t)(p.M * K * 2));
+  const __amdgpu_buffer_rsrc_t wr = wave_rsrc(W, (uint32_t)(p.N * K * 2));
+  const __amdgpu_buffer_rsrc_t yr = wave_rsrc(p.yref, (uint32_t)(p.M * p.N * 2));
+
+  // K-tile DMA sources: wave w fills 1 KiB blocks w*8 + u of each operand's 32 KiB tile part (8
+  // rows of 128 B); lane l writes row 64 w + 8 u + (l >> 3), stored chunk l & 7 = source chunk
+  // c ^ ((row >> 1) & 7).  The instruction offset carries the block step (u % 4) KiB: subtracted here.
+  unsigned xo[8], wo[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int r = 64 * wave + 8 * u + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t row = m0 + r < p.M ? m0 + r : p.M - 1;
+    const int64_t col = n0 + r < p.N ? n0 + r : p.N - 1;
+    xo[u] = (unsigned)((row * K + 8 * c) * 2) - (unsigned)((u % 4) * 1024);
+    wo[u] = (unsigned)((col * K + 8 * c) * 2) - (unsigned)((u % 4) * 1024);
+  }
+  // fragment reads: row 16 i + fr of the wave's block, 16-byte chunk 4 s + fq of k-half s
+  const int fr = lane & 15, fq = lane >> 4;
+  const unsigned lds0 = (unsigned)(uintptr_t)lds;
+  const unsigned lt0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) << 4);
+  const unsigned lt1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) << 4);
+  const unsigned xb0 = lds0 + wm * 16384 + lt0, xb1 = lds0 + wm * 16384 + lt1;
+  const unsigned wb0 = lds0 + 32768 + wn * 16384 + lt0, wb1 = lds0 + 32768 + wn * 16384 + lt1;
+  const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + wave * 8192);
+  const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
+  unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)(K / 64 - 2));
+  // reference-tile DMA sources: half h (rows 128 h ..) lands in slot (K / 64 + h) % 2; wave w
+  // fills rows 32 w + 2 u + (l >> 5), u = 0..15, row r's 16-byte chunk c at c ^ (r & 15)
+  const unsigned yrb = __builtin_amdgcn_readfirstlane((unsigned)(((m0 + 32 * wave) * p.N + n0) * 2));
+  const unsigned yh = __builtin_amdgcn_readfirstlane((unsigned)(128 * p.N * 2));
+  const unsigned ys2 = __builtin_amdgcn_readfirstlane((unsigned)(2 * p.N * 2));
+  const unsigned m0yb = __builtin_amdgcn_readfirstlane(lds0 + wave * 16384);
+  unsigned yo[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
+  unsigned koff, kc, m0s, sdma, srd, m0y, yso;
+#define MTQ_W4_ASM(BODY)                                                                              \
+  asm volatile(BODY                                                                                   \
+               : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
+                 [cnt] "+s"(cnt), [m0y] "=&s"(m0y), [yso] "=&s"(yso)                                     \
+               : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast),                         \
+                 [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]),                  \
+                 [xo4] "v"(xo[4]), [xo5] "v"(xo[5]), [xo6] "v"(xo[6]), [xo7] "v"(xo[7]),                  \
+                 [wo0] "v"(wo[0]), [wo1] "v"(wo[1]), [wo2] "v"(wo[2]), [wo3] "v"(wo[3]),                  \
+                 [wo4] "v"(wo[4]), [wo5] "v"(wo[5]), [wo6] "v"(wo[6]), [wo7] "v"(wo[7]),                  \
+                 [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1),                           \
+                 [yr] "s"(yr), [yrb] "s"(yrb), [yh] "s"(yh), [ys2] "s"(ys2), [m0yb] "s"(m0yb),             \
+                 [yo0] "v"(yo[0]), [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]),                  \
+                 [yo4] "v"(yo[4]), [yo5] "v"(yo[5]), [yo6] "v"(yo[6]), [yo7] "v"(yo[7])                   \
+               : MTQ_W4_CLOBBERS)
+  if constexpr (sizeof(T) == 2 && __is_same(T, __bf16))
+    MTQ_W4_ASM(MTQ_W4_BODY_BF16);
+  else
+    MTQ_W4_ASM(MTQ_W4_BODY_F16);
+#undef MTQ_W4_ASM
+
+  // ---- epilogue.  A lane's accumulators of tile (i, j) are out[m][n .. n+3], m = 16 i + fr, n =
+  // 16 j + 4 fq of the wave's block (a[32 i + 4 j ..]); bias, output and difference rounded to T,
+  // fp32 square-sum in a fixed order; the reference values from the LDS copy.
+  const T *Bi = reinterpret_cast<const T *>(p.bias);
+  const unsigned yslot = (unsigned)(((K / 64 + wm) & 1) * 65536);
+  float bj[8][4];
+  bool cok[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t c = n0 + wn * 128 + 16 * j + 4 * fq;
+    cok[j] = c < p.N;  // N % 8 == 0: the 4 columns are all in or all out
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bj[j][e] = HAS_BIAS ? Elem<T>::ld(Bi[cok[j] ? c + e : e]) : 0.f;
+  }
+  float sum = 0.f;
+  float o[32];
+#define MTQ_W4_EPI(I)                                                                                 \
+  {                                                                                                   \
+    MTQ_W4_STRIP_##I(o);                                                                              \
+    const bool rok = m0 + wm * 128 + 16 * (I) + fr < p.M;                                             \
+    const int rr = 16 * (I) + fr;                                                                     \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                   \
+      const int cl = wn * 128 + 16 * j + 4 * fq;                                                      \
+      T yv[4];                                                                                        \
+      __builtin_memcpy(yv, lds + yslot + rr * 512 + (((cl >> 3) ^ fr) << 4) + (cl & 7) * 2, 8);       \
+      const bool ok = rok && cok[j];                                                                  \
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                 \
+        const float y = Elem<T>::ld(Elem<T>::st(o[4 * j + e] + bj[j][e]));                            \
+        const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yv[e])));                             \
+        sum = ok ? __builtin_fmaf(d, d, sum) : sum;                                                   \
+      }                                                                                               \
+    }                                                                                                 \
+  }
+  MTQ_W4_EPI(0) MTQ_W4_EPI(1) MTQ_W4_EPI(2) MTQ_W4_EPI(3) MTQ_W4_EPI(4) MTQ_W4_EPI(5) MTQ_W4_EPI(6) MTQ_W4_EPI(7)
+#undef MTQ_W4_EPI
+  __syncthreads();
+#pragma unroll
+  for (int o2 = 32; o2 >= 1; o2 >>= 1) sum += __shfl_xor(sum, o2);
+  float *red = reinterpret_cast<float *>(lds);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  if (tid == 0) p.partial[(int64_t)g * p.tiles_m * p.tiles_n + tile] = red[0] + red[1] + red[2] + red[3];
+}
+
 // xs[g, m, k] = T(x[m, k] * sinv[g, k]) for all g: one read of x, G writes (the reference's
 // `inputs * pre_quant_scale` per alpha, tensor_quantizer.py:1143-1144).  GT > 0: the alpha count
 // as a compile-time constant, so every sinv load of the thread is issued before the first product
@@ -492,10 +633,11 @@ extern "C" int64_t mtq_awq_search_gemm_workspace_floats(int64_t M, int64_t N, in
   return partial_floats(M, N, G) + (G * M * K + 1) / 2;  // + xs [G, M, K] in 16-bit elements
 }
 
-extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const void *bias,
-                                   const void *yref, int64_t M, int64_t N, int64_t K, int dtype,
-                                   int G, float *loss, float *workspace, int64_t workspace_floats,
-                                   hipStream_t stream) {
+extern "C" int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const void *wq, const void *bias,
+                                          const void *yref, int64_t M, int64_t N, int64_t K, int dtype,
+                                          int G, float *loss, float *workspace, int64_t workspace_floats,
+                                          int kernel, hipStream_t stream) {
+  if (kernel < MTQ_AWQ_SEARCH_AUTO || kernel > MTQ_AWQ_SEARCH_W4) return MTQ_ERR_INVALID_ARG;
   if (M < 1 || N < 1 || K < kBK || K % kBK != 0 || G < 1 || G > 64) return MTQ_ERR_INVALID_ARG;
   if (!x || !sinv || !wq || !yref || !loss || !workspace) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
@@ -519,6 +661,22 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
   // 32 slots per 8 x 4 tile unit, units padded to a multiple of the 8 XCDs (see the kernel)
   const int64_t units = (int64_t)G * ((tiles_m + 7) / 8) * ((tiles_n + 3) / 4);
   const dim3 grid((unsigned)((units + 7) / 8 * 8 * 32));
+  const bool w4_ok = K >= 128 && M * N * 2 < ((int64_t)1 << 32);
+  if (kernel == MTQ_AWQ_SEARCH_W4 && !w4_ok) return MTQ_ERR_INVALID_ARG;
+  if (kernel == MTQ_AWQ_SEARCH_W4) {
+    count_dispatch(kDispAwqSearchW4);
+    if (dtype == MTQ_BF16) {
+      if (bias)
+        awq_search_w4_kernel<__bf16, true><<<grid, 256, 0, stream>>>(a);
+      else
+        awq_search_w4_kernel<__bf16, false><<<grid, 256, 0, stream>>>(a);
+    } else {
+      if (bias)
+        awq_search_w4_kernel<_Float16, true><<<grid, 256, 0, stream>>>(a);
+      else
+        awq_search_w4_kernel<_Float16, false><<<grid, 256, 0, stream>>>(a);
+    }
+  } else {
   count_dispatch(kDispAwqSearchPp);
   if (dtype == MTQ_BF16) {
     if (bias)
@@ -531,11 +689,20 @@ extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *
     else
       awq_search_pp_kernel<_Float16, false><<<grid, kThreads, 0, stream>>>(a);
   }
+  }
   int st = host_check_launch();
   if (st != MTQ_OK) return st;
   awq_search_finish_kernel<<<(unsigned)G, 256, 0, stream>>>(workspace, (int)tiles, G, 1.0 / ((double)M * (double)N),
                                                   loss);
   return host_check_launch();
+}
+
+extern "C" int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const void *bias,
+                                   const void *yref, int64_t M, int64_t N, int64_t K, int dtype,
+                                   int G, float *loss, float *workspace, int64_t workspace_floats,
+                                   hipStream_t stream) {
+  return mtq_awq_search_gemm_kernel(x, sinv, wq, bias, yref, M, N, K, dtype, G, loss, workspace, workspace_floats,
+                                    MTQ_AWQ_SEARCH_AUTO, stream);
 }
 
 extern "C" int64_t mtq_awq_mse_multi_workspace_floats(int64_t n, int G) {

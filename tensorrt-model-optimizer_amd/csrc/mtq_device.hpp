@@ -473,7 +473,7 @@ enum DispatchId {
   kDispEwVec, kDispEwGroupSk, kDispEwGroup, kDispEwRowwave, kDispAmaxPersist, kDispAmaxRowsU,
   kDispAmaxRowsShort, kDispAmaxColsWide, kDispBlockQuantDyn, kDispHistValue, kDispHistValueChunked,
   kDispMxVec, kDispMxE2m1Native, kDispNvfp4NativeU, kDispAwqSearchPp, kDispAwqPrescale, kDispAwqMseMulti,
-  kDispHistValueNz, kDispMxE4m3Native, kDispCount
+  kDispHistValueNz, kDispMxE4m3Native, kDispAwqSearchW4, kDispCount
 };
 void count_dispatch(int id);
 

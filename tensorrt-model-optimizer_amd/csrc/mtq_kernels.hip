@@ -3216,7 +3216,7 @@ void count_dispatch(int id) { g_dispatch[id].fetch_add(1, std::memory_order_rela
 static const char *const kDispatchNames[kDispCount] = {
     "ew_vec", "ew_group_sk", "ew_group", "ew_rowwave", "amax_persist", "amax_rows_u", "amax_rows_short",
     "amax_cols_wide", "block_quant_dyn", "hist_value", "hist_value_chunked", "mx_vec", "mx_e2m1_native",
-    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_value_nz", "mx_e4m3_native"};
+    "nvfp4_native_u", "awq_search_pp", "awq_prescale", "awq_mse_multi", "hist_value_nz", "mx_e4m3_native", "awq_search_w4"};
 }  // namespace mtq
 
 // ============================================================================================

@@ -468,7 +468,8 @@ void mse_accumulate(const at::Tensor &a, const at::Tensor &b, at::Tensor loss, i
 // AWQ-lite alpha search, all alphas of one linear in one MFMA launch (mtq_awq_search_gemm):
 // loss[g] += mean((T(T(x * sinv[g]) @ wq[g]^T + bias) - yref)^2), the GEMM output never stored.
 void awq_search_gemm(const at::Tensor &x, const at::Tensor &sinv, const at::Tensor &wq,
-                     const c10::optional<at::Tensor> &bias, const at::Tensor &yref, at::Tensor loss) {
+                     const c10::optional<at::Tensor> &bias, const at::Tensor &yref, at::Tensor loss,
+                     int64_t kernel) {
   check_device(x, "x");
   check_device(wq, "wq");
   check_device(yref, "yref");
@@ -495,10 +496,10 @@ void awq_search_gemm(const at::Tensor &x, const at::Tensor &sinv, const at::Tens
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t wf = mtq_awq_search_gemm_workspace_floats(M, N, K, (int)G);
   at::Tensor ws = at::empty({std::max<int64_t>(wf, 1)}, x.options().dtype(at::kFloat));
-  int st = mtq_awq_search_gemm(xc.data_ptr(), sc.data_ptr(), wc.data_ptr(),
-                               b.defined() ? b.data_ptr() : nullptr, yc.data_ptr(), M, N, K, dt,
-                               (int)G, loss.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(),
-                               cur_stream(xc));
+  int st = mtq_awq_search_gemm_kernel(xc.data_ptr(), sc.data_ptr(), wc.data_ptr(),
+                                      b.defined() ? b.data_ptr() : nullptr, yc.data_ptr(), M, N, K, dt,
+                                      (int)G, loss.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(),
+                                      (int)kernel, cur_stream(xc));
   check_status(st, "awq_search_gemm");
 }
 
@@ -1222,7 +1223,8 @@ TORCH_LIBRARY(modelopt_amd, m) {
   m.def("col_mean(Tensor x, bool absval) -> Tensor");
   m.def("awq_scale_table(Tensor x_max, Tensor w_max, Tensor e_num, Tensor e_den) -> Tensor");
   m.def("awq_mse_multi(Tensor out, Tensor ref, Tensor(a!) loss) -> ()");
-  m.def("awq_search_gemm(Tensor x, Tensor sinv, Tensor wq, Tensor? bias, Tensor yref, Tensor(a!) loss) -> ()");
+  m.def("awq_search_gemm(Tensor x, Tensor sinv, Tensor wq, Tensor? bias, Tensor yref, Tensor(a!) loss, "
+        "int kernel=0) -> ()");
   m.def("nvfp4_fake_quant_block(Tensor inputs, Tensor global_amax, int block_size=16) -> Tensor");
   m.def("set_disable_triton_kernel(bool disable) -> ()", &set_disable_triton_kernel);
   m.def("fp4_block_scale_quant(Tensor inputs, Tensor scales) -> Tensor");

@@ -13,6 +13,10 @@ without storing the GEMM output.  Checks:
   few outputs by one bf16 ulp; the bound is stated here and is far below the 10-100 % spread
   between the alphas' losses that the search ranks;
 * the weight side ``block_quant_dynamic_multi`` equals G single-alpha launches bit for bit.
+Both search kernels run every check: ``kernel=1`` the r03 ping-pong kernel (8 waves), ``kernel=2``
+the r06 one-wave-per-SIMD kernel whose K loop is generated inline asm (scripts/gen_awq_w4.py; K >=
+128); ``kernel=0`` (what the product calls) is the first, the faster one at the widths the fused
+search serves.
 """
 
 import pytest
@@ -43,11 +47,15 @@ def _host_loss(x, sinv, wq, bias, yref):
     return torch.tensor(out, dtype=torch.float64).float()
 
 
+@pytest.mark.parametrize("kernel", [1, 2])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("shape", [(256, 256, 64), (300, 320, 192), (512, 768, 256), (37, 1024, 128)])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (300, 320, 192), (512, 768, 256), (37, 1024, 128),
+                                   (1000, 520, 640)])
 @pytest.mark.parametrize("with_bias", [False, True])
-def test_exact_integer_data(gpu, dtype, shape, with_bias):
+def test_exact_integer_data(gpu, dtype, shape, with_bias, kernel):
     M, N, K = shape
+    if kernel == 2 and K < 128:
+        pytest.skip("the W4 kernel needs K >= 128 (test_kernel_choice covers the rejection)")
     G = 3
     g = torch.Generator().manual_seed(M + N + K)
     # sparse small integers: every product sum, output, difference and square sum (per lane,
@@ -62,17 +70,18 @@ def test_exact_integer_data(gpu, dtype, shape, with_bias):
     yref = torch.randint(-4, 5, (M, N), generator=g).to(dtype)
     loss = torch.zeros(G, device=gpu)
     ops().awq_search_gemm(x.to(gpu), sinv.to(gpu), wq.to(gpu), None if bias is None else bias.to(gpu),
-                          yref.to(gpu), loss)
+                          yref.to(gpu), loss, kernel)
     want = _host_loss(x, sinv, wq, bias, yref)
     assert torch.equal(loss.cpu(), want), (loss.cpu(), want)
     # accumulates (loss[g] += ...) and is deterministic
     ops().awq_search_gemm(x.to(gpu), sinv.to(gpu), wq.to(gpu), None if bias is None else bias.to(gpu),
-                          yref.to(gpu), loss)
+                          yref.to(gpu), loss, kernel)
     assert torch.equal(loss.cpu(), want + want)
 
 
+@pytest.mark.parametrize("kernel", [1, 2])
 @pytest.mark.parametrize("nk", [(1024, 4096), (4096, 4096), (14336, 4096), (4096, 14336)])
-def test_llama_shapes_vs_unfused(gpu, nk):
+def test_llama_shapes_vs_unfused(gpu, nk, kernel):
     N, K = nk
     M, G = 512, 4
     dt = torch.bfloat16
@@ -87,12 +96,41 @@ def test_llama_shapes_vs_unfused(gpu, nk):
         assert torch.equal(wq[gi], ops().block_quant_dynamic(w, pqs_w[gi], 128, 4, False, False))
     yref = F.linear(x, w, bias)
     loss = torch.zeros(G, device=gpu)
-    ops().awq_search_gemm(x, sinv, wq, bias, yref, loss)
+    ops().awq_search_gemm(x, sinv, wq, bias, yref, loss, kernel)
     want = torch.stack([(F.linear(x * sinv[gi], wq[gi], bias) - yref).float().pow(2).mean() for gi in range(G)])
     torch.testing.assert_close(loss, want, rtol=2e-3, atol=0)
     again = torch.zeros(G, device=gpu)
-    ops().awq_search_gemm(x, sinv, wq, bias, yref, again)
+    ops().awq_search_gemm(x, sinv, wq, bias, yref, again, kernel)
     assert torch.equal(loss, again)  # deterministic
+    # the two kernels hold the same fp32 accumulators (same MFMA k order); only the per-tile
+    # square-sum order differs
+    other = torch.zeros(G, device=gpu)
+    ops().awq_search_gemm(x, sinv, wq, bias, yref, other, 3 - kernel)
+    torch.testing.assert_close(loss, other, rtol=1e-5, atol=0)
+
+
+def test_kernel_choice(gpu):
+    """kernel=0 (the product call) runs the ping-pong kernel, kernel=2 the W4 kernel; asking for W4
+    at K = 64 is an error, not a silent fallback."""
+    from modelopt_amd import _ext as ext
+
+    dt = torch.bfloat16
+    for K, kernel, want in ((64, 0, "awq_search_pp"), (4096, 0, "awq_search_pp"), (128, 2, "awq_search_w4"),
+                            (4096, 2, "awq_search_w4"), (4096, 1, "awq_search_pp")):
+        x = torch.randn(256, K, device=gpu).to(dt)
+        wq = torch.randn(2, 256, K, device=gpu).to(dt)
+        sinv = torch.ones(2, K, device=gpu, dtype=dt)
+        before = ext.dispatch_counts()
+        ops().awq_search_gemm(x, sinv, wq, None, torch.zeros(256, 256, device=gpu, dtype=dt),
+                              torch.zeros(2, device=gpu), kernel)
+        torch.cuda.synchronize()
+        after = ext.dispatch_counts()
+        grown = {k for k in after if after[k] > before.get(k, 0)}
+        assert want in grown and ({"awq_search_pp", "awq_search_w4"} - {want}).isdisjoint(grown), (K, grown)
+    with pytest.raises(RuntimeError):
+        ops().awq_search_gemm(torch.zeros(256, 64, device=gpu, dtype=dt), torch.ones(2, 64, device=gpu, dtype=dt),
+                              torch.zeros(2, 256, 64, device=gpu, dtype=dt), None,
+                              torch.zeros(256, 256, device=gpu, dtype=dt), torch.zeros(2, device=gpu), 2)
 
 
 def test_rejects_unsupported(gpu):
