@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
     unsigned koff, kc, m0s, sdma, srd;
     unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)(K / 64));
     const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
-    if constexpr (EPI == 2) {
+    if constexpr (EPI >= 2) {
       // the reference tile rides in the last two K tiles' DMAs (gen_w4asm.py body_t64y): half h
       // (rows 128 h ..) lands in slot (K / 64 + h) % 2, row r's 16-byte chunk c at c ^ (r & 15)
       const __amdgpu_buffer_rsrc_t yr = rsrc_of(p.yref, (uint32_t)(p.M * p.N * 2));
@@ -95,7 +95,8 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
       for (int k = 0; k < 8; ++k)
         yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
       unsigned m0y, yso;
-      unsigned cnt2 = __builtin_amdgcn_readfirstlane((unsigned)(K / 64 - 2));
+      // EPI 3 (T64B): the loop runs two tiles per pass (K % 128 == 0)
+      unsigned cnt2 = __builtin_amdgcn_readfirstlane((unsigned)(EPI == 3 ? (K / 64 - 2) / 2 : K / 64 - 2));
 #define W4_ASMY(BODY) \
       asm volatile(BODY \
                    : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
@@ -112,9 +113,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
                    : W4ASM_CLOBBERS)
       if constexpr (V == 0) W4_ASMY(W4ASM_BODY_Y_0);
       if constexpr (V == 1) W4_ASMY(W4ASM_BODY_Y_1);
-      if constexpr (V == 2) W4_ASMY(W4ASM_BODY_Y_2);
-      if constexpr (V == 3) W4_ASMY(W4ASM_BODY_Y_3);
-      if constexpr (V == 4) W4_ASMY(W4ASM_BODY_Y_4);
+
 #undef W4_ASMY
     }
 #define W4_ASM64(BODY)                                                                               \
@@ -128,7 +127,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
                  [wo4] "v"(wo[4]), [wo5] "v"(wo[5]), [wo6] "v"(wo[6]), [wo7] "v"(wo[7]),                  \
                  [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1)                           \
                : W4ASM_CLOBBERS)
-    static_assert(EPI == 2, "the reference-prefetch epilogue only");
+    static_assert(EPI >= 2, "the reference-prefetch epilogue only");
 #undef W4_ASM64
   }
   const int fr = lane & 15, fq = lane >> 4;
@@ -150,7 +149,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
       const int64_t off = (ok ? m : 0) * p.N + (ok ? n : 0);                                         \
       if constexpr (EPI == 1) {                                                                      \
         __builtin_memset(yr, 0, 8);                                                                  \
-      } else if constexpr (EPI == 2) {                                                               \
+      } else if constexpr (EPI >= 2) {                                                               \
         const int rr = 16 * (I) + fr, cl = wn * 128 + 16 * j + 4 * fq;                               \
         __builtin_memcpy(yr, lds + yslot + rr * 512 + (((cl >> 3) ^ fr) << 4) + (cl & 7) * 2, 8);    \
       } else {                                                                                       \
@@ -186,14 +185,11 @@ template <int V> int go(const Args &a, hipStream_t stream) {
 // var: gen_w4asm.py VARIANTS index
 extern "C" int awq_w4asm(int var, const void *xs, const void *wq, const void *yref, float *partial, int64_t M, int64_t N,
                          int64_t K, int G, hipStream_t stream) {
-  if (K % 64 || K < 128 || N % 8) return 2;
+  if (K % 128 || K < 128 || N % 8) return 2;
   Args a{xs, wq, yref, partial, M, N, K, (int)((M + 255) / 256), (int)((N + 255) / 256), G};
   switch (var) {
   case 0: return go<0>(a, stream);
   case 1: return go<1>(a, stream);
-  case 2: return go<2>(a, stream);
-  case 3: return go<3>(a, stream);
-  case 4: return go<4>(a, stream);
   default: return 3;
   }
 }

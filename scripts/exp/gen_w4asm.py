@@ -31,12 +31,10 @@ SLOT = 32768
 # C++-side fields (kW4Epi / kW4Gm): EPI 1 = probe without the reference-tile loads; GM = row tiles
 # per XCD tile unit (the product's 8 x 4 units: GM 8)
 # EPI 2: the reference tile prefetched into the LDS ring by the last two K tiles (body_t64y)
+# EPI 3: T64B (three fragment sets, two barriers per tile, DMAs two tiles ahead from the tile start)
 VARIANTS = [
-    (2, "G", 2, 0, 1, "", 2, 8),
-    (2, "I", 2, 0, 1, "", 2, 8),
-    (2, "J", 2, 0, 1, "", 2, 8),
     (2, "K", 2, 0, 1, "", 2, 8),
-    (2, "G", 2, 0, 1, "sc1", 2, 8),
+    (2, "B3", 2, 0, 1, "", 3, 8),
 ]
 CACHE = ""
 
@@ -257,6 +255,84 @@ def body_t64y(order, probe):
     return L
 
 
+# ---- T64B: three fragment sets (A = v[64:127] k-half 0, B / C = v[128:191] / v[192:255] k-half 1
+# of alternate tiles); a tile's fragments are all read during the previous tile's phase 2, so its
+# slot is free at that tile's end barrier and the DMAs two tiles ahead are issued in phase 1:
+#   phase 1: MFMAs on A (k0 of t) + the 16 DMAs of tile t+2 into slot t % 2;
+#   vmcnt(16) (tile t+1 landed) + s_barrier;
+#   phase 2: MFMAs on K1 (k1 of t) + 32 reads of tile t+1 (k0 -> A, k1 -> the other k1 set);
+#   lgkmcnt(0) + s_barrier.
+def xf3(s, i):
+    return (64, 128, 192)[s] + 4 * i
+
+
+def wf3(s, j):
+    return (64, 128, 192)[s] + 32 + 4 * j
+
+
+def mfma3(s, i, j):
+    a = (i * 8 + j) * 4
+    return (f"v_mfma_f32_16x16x32_bf16 a[{a}:{a + 3}], v[{wf3(s, j)}:{wf3(s, j) + 3}], "
+            f"v[{xf3(s, i)}:{xf3(s, i) + 3}], a[{a}:{a + 3}]")
+
+
+def reads3(s, xb, wb):
+    out = []
+    for i in range(8):
+        out.append(f"ds_read_b128 v[{xf3(s, i)}:{xf3(s, i) + 3}], {xb} offset:{i * 2048}")
+        out.append(f"ds_read_b128 v[{wf3(s, i)}:{wf3(s, i) + 3}], {wb} offset:{i * 2048}")
+    return out
+
+
+def tile3(k1set, yhalf=None):
+    nk1 = 3 - k1set  # the next tile's k-half-1 set (B <-> C)
+    L = ["s_add_u32 %[m0s], %[m0b], %[sdma]"] if yhalf is None else \
+        ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
+         "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
+    if yhalf is None:
+        L += ["s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128"]
+        dm = dmas64("%[m0s]", False)
+    else:
+        dm = ydmas()
+    for n in range(64):
+        L.append(mfma3(0, n // 8, n % 8))
+        if n % 4 == 1:
+            L += dm[n // 4]
+    L += ["s_waitcnt vmcnt(16)", "s_barrier",
+          "s_xor_b32 %[srd], %[sdma], 65536",
+          "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
+          "v_add_u32 v62, %[srd], %[xb1]", "v_add_u32 v63, %[srd], %[wb1]"]
+    rd = reads3(0, "v60", "v61") + reads3(nk1, "v62", "v63")
+    for n in range(64):
+        L.append(mfma3(k1set, n // 8, n % 8))
+        if n % 2 == 0:
+            L.append(rd[n // 2])
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
+    return L
+
+
+def body_t64b():
+    L = ["s_nop 4"]
+    L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    L += ["s_mov_b32 %[koff], 0", "s_mov_b32 %[sdma], 0"]
+    for t in range(2):
+        L += ["s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128",
+              f"s_add_u32 %[m0s], %[m0b], {t * 65536}"]
+        for d in dmas64("%[m0s]", True):
+            L += d
+    L += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    L += reads3(0, "%[xb0]", "%[wb0]") + reads3(1, "%[xb1]", "%[wb1]")
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]  # slot 0 free for tile 2's DMAs
+    L += ["s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_tail_%="]
+    L.append("L_w4_loop_%=:")
+    L += tile3(1) + tile3(2)
+    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_loop_%="]
+    L.append("L_w4_tail_%=:")
+    L += tile3(1, 0) + tile3(2, 1)
+    L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier", "s_nop 15", "s_nop 15", "s_nop 15"]
+    return L
+
+
 def body_t64(order, probe):
     L = ["s_nop 4"]
     L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
@@ -314,12 +390,14 @@ def main():
     text = "// generated by scripts/exp/gen_w4asm.py -- do not edit\n"
     global CACHE
     for v, (S, order, swz, probe, ofs, CACHE, _epi, _gm) in enumerate(VARIANTS):
-        if S == 2:
+        if S == 2 and _epi == 3:
+            lines = body_t64b()
+        elif S == 2:
             lines = body_t64y(order, probe) if _epi == 2 else body_t64(order, probe)
         else:
             lines = body(S, order, probe, ofs)
         asm = "".join(f'  "{ln}\\n\\t"\n' for ln in lines)
-        name = f"W4ASM_BODY_{v}" if _epi != 2 else f"W4ASM_BODY_Y_{v}"
+        name = f"W4ASM_BODY_{v}" if _epi < 2 else f"W4ASM_BODY_Y_{v}"
         text += f"#define {name} \\\n" + asm.replace("\n", " \\\n") + "\n"
     text += f"#define W4ASM_NVAR {len(VARIANTS)}\n"
     text += "constexpr int kW4Slots[] = {" + ", ".join(str(v[0]) for v in VARIANTS) + "};\n"
@@ -327,7 +405,7 @@ def main():
     text += "constexpr int kW4Ofs[] = {" + ", ".join(str(v[4]) for v in VARIANTS) + "};\n"
     text += "constexpr int kW4Epi[] = {" + ", ".join(str(v[6]) for v in VARIANTS) + "};\n"
     text += "constexpr int kW4Gm[] = {" + ", ".join(str(v[7]) for v in VARIANTS) + "};\n"
-    clob = ", ".join(f'"v{r}"' for r in range(120, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
+    clob = ", ".join(f'"v{r}"' for r in range(60, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
     text += "#define W4ASM_CLOBBERS " + clob.replace("\n", " \\\n") + ', "memory", "scc"\n'
     text += strips()
     OUT.write_text(text)
