@@ -381,11 +381,10 @@ int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const v
                         float *loss, float *workspace, int64_t workspace_floats,
                         hipStream_t stream);
 /* The same with the search kernel named (for A/B and tests; same arguments and results up to the
- * per-tile square-sum order): MTQ_AWQ_SEARCH_AUTO = what mtq_awq_search_gemm runs (PP, the faster
- * one on the widths the fused search serves); PP = the r03 two-group ping-pong kernel (8 waves,
- * 128 x 64 per wave);
+ * per-tile square-sum order): MTQ_AWQ_SEARCH_AUTO = what mtq_awq_search_gemm runs (W4 where its
+ * limits allow, else PP); PP = the r03 two-group ping-pong kernel (8 waves, 128 x 64 per wave);
  * W4 = the r06 one-wave-per-SIMD kernel (4 waves, 128 x 128 per wave, K loop in generated inline
- * asm; needs K >= 128 and M * N * 2 < 2^32, MTQ_ERR_INVALID_ARG otherwise). */
+ * asm; needs K % 128 == 0 and M * N * 2 < 2^32, MTQ_ERR_INVALID_ARG otherwise). */
 enum { MTQ_AWQ_SEARCH_AUTO = 0, MTQ_AWQ_SEARCH_PP = 1, MTQ_AWQ_SEARCH_W4 = 2 };
 int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const void *wq, const void *bias,
                                const void *yref, int64_t M, int64_t N, int64_t K, int dtype, int G,

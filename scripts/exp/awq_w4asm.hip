@@ -113,6 +113,10 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
                    : W4ASM_CLOBBERS)
       if constexpr (V == 0) W4_ASMY(W4ASM_BODY_Y_0);
       if constexpr (V == 1) W4_ASMY(W4ASM_BODY_Y_1);
+      if constexpr (V == 2) W4_ASMY(W4ASM_BODY_Y_2);
+      if constexpr (V == 3) W4_ASMY(W4ASM_BODY_Y_3);
+      if constexpr (V == 4) W4_ASMY(W4ASM_BODY_Y_4);
+      if constexpr (V == 5) W4_ASMY(W4ASM_BODY_Y_5);
 
 #undef W4_ASMY
     }
@@ -190,6 +194,10 @@ extern "C" int awq_w4asm(int var, const void *xs, const void *wq, const void *yr
   switch (var) {
   case 0: return go<0>(a, stream);
   case 1: return go<1>(a, stream);
+  case 2: return go<2>(a, stream);
+  case 3: return go<3>(a, stream);
+  case 4: return go<4>(a, stream);
+  case 5: return go<5>(a, stream);
   default: return 3;
   }
 }

@@ -33,8 +33,12 @@ SLOT = 32768
 # EPI 2: the reference tile prefetched into the LDS ring by the last two K tiles (body_t64y)
 # EPI 3: T64B (three fragment sets, two barriers per tile, DMAs two tiles ahead from the tile start)
 VARIANTS = [
-    (2, "K", 2, 0, 1, "", 2, 8),
-    (2, "B3", 2, 0, 1, "", 3, 8),
+    (2, "spread/spread/0", 2, 0, 1, "", 3, 8),
+    (2, "front/spread/0", 2, 0, 1, "", 3, 8),
+    (2, "spread/front/0", 2, 0, 1, "", 3, 8),
+    (2, "front/front/0", 2, 0, 1, "", 3, 8),
+    (2, "spread/spread/1", 2, 0, 1, "", 3, 8),
+    (2, "spread/spread/2", 2, 0, 1, "", 3, 8),
 ]
 CACHE = ""
 
@@ -284,20 +288,28 @@ def reads3(s, xb, wb):
     return out
 
 
+B3_READS = "spread"   # "spread": one per 2 MFMAs; "front": one per MFMA over the first 32
+B3_DMAS = "spread"    # "spread": one per 4 MFMAs; "front": one per 2 over the first 32
+B3_PROBE = 0          # 1: no K-tile DMAs in the loop; 2: they re-load tile 0 (L2 hits)
+
+
 def tile3(k1set, yhalf=None):
     nk1 = 3 - k1set  # the next tile's k-half-1 set (B <-> C)
     L = ["s_add_u32 %[m0s], %[m0b], %[sdma]"] if yhalf is None else \
         ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
          "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
     if yhalf is None:
-        L += ["s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128"]
-        dm = dmas64("%[m0s]", False)
+        L += ["s_min_u32 %[kc], %[koff], %[klast]" if B3_PROBE != 2 else "s_mov_b32 %[kc], 0",
+              "s_add_u32 %[koff], %[koff], 128"]
+        dm = dmas64("%[m0s]", False) if B3_PROBE != 1 else [[]] * 16
     else:
         dm = ydmas()
     for n in range(64):
         L.append(mfma3(0, n // 8, n % 8))
-        if n % 4 == 1:
+        if B3_DMAS == "spread" and n % 4 == 1:
             L += dm[n // 4]
+        if B3_DMAS == "front" and n < 32 and n % 2 == 0:
+            L += dm[n // 2]
     L += ["s_waitcnt vmcnt(16)", "s_barrier",
           "s_xor_b32 %[srd], %[sdma], 65536",
           "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
@@ -305,8 +317,10 @@ def tile3(k1set, yhalf=None):
     rd = reads3(0, "v60", "v61") + reads3(nk1, "v62", "v63")
     for n in range(64):
         L.append(mfma3(k1set, n // 8, n % 8))
-        if n % 2 == 0:
+        if B3_READS == "spread" and n % 2 == 0:
             L.append(rd[n // 2])
+        if B3_READS == "front" and n < 32:
+            L.append(rd[n])
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
     return L
 
@@ -391,6 +405,9 @@ def main():
     global CACHE
     for v, (S, order, swz, probe, ofs, CACHE, _epi, _gm) in enumerate(VARIANTS):
         if S == 2 and _epi == 3:
+            global B3_READS, B3_DMAS, B3_PROBE
+            B3_READS, B3_DMAS, pr = order.split("/")
+            B3_PROBE = int(pr)
             lines = body_t64b()
         elif S == 2:
             lines = body_t64y(order, probe) if _epi == 2 else body_t64(order, probe)

@@ -11,26 +11,29 @@ hipcc's waits collapse its prefetch; DESIGN.md §4e, measured in scripts/exp/awq
 * K tiles of 64: both operands by buffer_load_dwordx4 ... lds, 8 rows x 128 B per 1 KiB DMA (whole
   L2 lines), 16 DMAs per wave per tile, into two 64 KiB LDS slots (X rows then W rows, 128-byte
   rows, chunk c of row r at c ^ ((r >> 1) & 7): conflict-free ds_read_b128 for its lane groups);
-* fragments in VGPRs by k-half: set 0 = v[128:191] (k 0..31), set 1 = v[192:255] (k 32..63);
-* per tile: phase 1 = 64 MFMAs on set 0 while the 16 ds_read_b128 of k-half 1 fill set 1;
-  vmcnt(0) (this wave's DMAs of tile t+1 landed) + lgkmcnt(0) + s_barrier; phase 2 = 64 MFMAs on
-  set 1 while k-half 0 of tile t+1 fills set 0 and the 16 DMAs of tile t+2 go into this tile's
-  slot (free: every wave's reads of it finished before the barrier).  One barrier per tile, every
-  wait counted by hand;
+* three fragment sets in VGPRs: A = v[64:127] (k-half 0 of every tile), B / C = v[128:191] /
+  v[192:255] (k-half 1 of even / odd tiles); a tile's fragments are ALL read during the previous
+  tile's second phase, so its LDS slot is free from that tile's end and the DMAs two tiles ahead
+  get three MFMA phases to land (a two-set schedule freed the slot one phase later and gave them
+  one and a half: 5-9 % slower, scripts/exp/gen_w4asm.py);
+* per tile t: phase 1 = 64 MFMAs on A (k0 of t) with the 16 DMAs of tile t+2 into slot t % 2
+  (one per 4 MFMAs); vmcnt(16) (this wave's DMAs of tile t+1 landed) + s_barrier; phase 2 = 64
+  MFMAs on B|C (k1 of t) with the 32 ds_read_b128 of tile t+1 (k0 -> A, k1 -> the other of B|C)
+  one per MFMA over the first 32; lgkmcnt(0) + s_barrier.  Every wait counted by hand;
 * the last two tiles are peeled: their DMA slots carry the epilogue's reference (yref) tile, half
   h (rows 128 h ..) into slot (K / 64 + h) % 2 with the 16-byte chunk c of row r at c ^ (r & 15),
   so the epilogue reads it from LDS without a load round trip.
-The ring slots alternate at run time (an SGPR XOR per tile), so the loop body is one tile.
+The ring slots alternate at run time (an SGPR XOR per tile); the loop body is two tiles (the
+k-half-1 set alternates), so K % 128 == 0.
 """
 from pathlib import Path
 
 OUT = Path(__file__).resolve().parents[1] / "tensorrt-model-optimizer_amd" / "csrc" / "mtq_awq_w4.inc"
-SET_BASE = (128, 192)
+SET_BASE = (64, 128, 192)  # A, B, C
 MFMA = {"BF16": "v_mfma_f32_16x16x32_bf16", "F16": "v_mfma_f32_16x16x32_f16"}
-# phase-2 placement (after MFMA #): ds_reads of the next tile's k-half 0, DMAs of tile t+2
-P2_READS = [4 * k + 2 for k in range(16)]
-P2_DMAS = [4 * k for k in range(16)]
-P1_READS = [2 + 3 * k for k in range(16)]
+# placement (after MFMA #): phase-1 DMAs of tile t+2, phase-2 reads of tile t+1
+P1_DMAS = [4 * k + 1 for k in range(16)]
+P2_READS = list(range(32))
 
 
 def xf(s, i):
@@ -80,31 +83,29 @@ def ydmas():
     return out
 
 
-def tile(op, yhalf=None):
-    L = ["s_waitcnt lgkmcnt(0)", "v_add_u32 v120, %[sdma], %[xb1]", "v_add_u32 v121, %[sdma], %[wb1]"]
-    rd = reads(1, "v120", "v121")
-    for n in range(64):
-        L.append(mfma(op, 0, n // 8, n % 8))
-        if n in P1_READS:
-            L.append(rd[P1_READS.index(n)])
-    L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier",
-          "s_xor_b32 %[srd], %[sdma], 65536", "v_add_u32 v122, %[srd], %[xb0]", "v_add_u32 v123, %[srd], %[wb0]"]
+def tile(op, k1set, yhalf=None):
+    """One K tile: k-half 1 of this tile in set k1set (1 = B, 2 = C), the next tile's in the other."""
     if yhalf is None:
-        L += ["s_add_u32 %[m0s], %[m0b], %[sdma]", "s_min_u32 %[kc], %[koff], %[klast]",
-              "s_add_u32 %[koff], %[koff], 128"]
+        L = ["s_add_u32 %[m0s], %[m0b], %[sdma]", "s_min_u32 %[kc], %[koff], %[klast]",
+             "s_add_u32 %[koff], %[koff], 128"]
         dm = kdmas()
     else:
-        L += ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
-              "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
+        L = ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
+             "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
         dm = ydmas()
-    rd = reads(0, "v122", "v123")
     for n in range(64):
-        L.append(mfma(op, 1, n // 8, n % 8))
-        if n in P2_DMAS:
-            L += dm[P2_DMAS.index(n)]
+        L.append(mfma(op, 0, n // 8, n % 8))
+        if n in P1_DMAS:
+            L += dm[P1_DMAS.index(n)]
+    L += ["s_waitcnt vmcnt(16)", "s_barrier", "s_xor_b32 %[srd], %[sdma], 65536",
+          "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
+          "v_add_u32 v62, %[srd], %[xb1]", "v_add_u32 v63, %[srd], %[wb1]"]
+    rd = reads(0, "v60", "v61") + reads(3 - k1set, "v62", "v63")
+    for n in range(64):
+        L.append(mfma(op, k1set, n // 8, n % 8))
         if n in P2_READS:
             L.append(rd[P2_READS.index(n)])
-    L.append("s_xor_b32 %[sdma], %[sdma], 65536")
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
     return L
 
 
@@ -118,14 +119,14 @@ def body(op):
         for d in kdmas():
             L += d
     L += ["s_waitcnt vmcnt(16)", "s_barrier"]
-    L += reads(0, "%[xb0]", "%[wb0]")
+    L += reads(0, "%[xb0]", "%[wb0]") + reads(1, "%[xb1]", "%[wb1]")
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]  # slot 0 free for tile 2's DMAs
     L += ["s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_tail_%="]  # K = 128: the two peeled tiles only
     L.append("L_w4_loop_%=:")
-    L += tile(op)
+    L += tile(op, 1) + tile(op, 2)
     L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_loop_%="]
     L.append("L_w4_tail_%=:")
-    L += tile(op, 0)
-    L += tile(op, 1)
+    L += tile(op, 1, 0) + tile(op, 2, 1)
     # every DMA landed on every wave before the epilogue reads the yref tile; MFMA results settle
     # before the accumulator reads that follow the statement
     L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier", "s_nop 15", "s_nop 15", "s_nop 15"]
@@ -137,7 +138,7 @@ def text():
     for key, op in MFMA.items():
         asm = "".join(f'  "{ln}\\n\\t"\n' for ln in body(op))
         t += f"#define MTQ_W4_BODY_{key} \\\n" + asm.replace("\n", " \\\n") + "\n"
-    clob = ", ".join(f'"v{r}"' for r in range(120, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
+    clob = ", ".join(f'"v{r}"' for r in range(60, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
     t += "#define MTQ_W4_CLOBBERS " + clob.replace("\n", " \\\n") + ', "memory", "scc"\n'
     for i in range(8):  # the 32 accumulators of row block i into float o[32]
         rd = " ".join(f'asm volatile("v_accvgpr_read_b32 %0, a{32 * i + r}" : "=v"(o[{r}]));' for r in range(32))

@@ -377,10 +377,9 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
 // hand and the compiler sees one opaque statement that names the VGPRs v[120:255] and all AGPRs
 // it uses.  Same tile order, operands, roundings and loss as awq_search_pp_kernel (a different
 // per-tile square-sum order).  Requires K % 64 == 0, K >= 128 and M * N * 2 < 2^32 (32-bit buffer
-// offsets of the reference tile).  Measured against the pp kernel (kernel time, 8192 tokens, 11
-// alphas; profiles/r06/awq/): gate 7.56 vs 7.97 ms, but k / q / down 0.66 / 2.25 / 7.62 vs 0.61 /
-// 2.20 / 7.55 ms -- so the product (MTQ_AWQ_SEARCH_AUTO) keeps the pp kernel, which is what the
-// fused path runs (N <= 2048, k / v_proj); this one is selected explicitly (kernel = W4).
+// offsets of the reference tile); otherwise the launcher runs the pp kernel.  Kernel time at 8192
+// tokens x 11 alphas (profiles/r06/awq/): k / q / gate / down 0.61 / 2.10 / 7.28 / 7.42 ms against
+// the pp kernel's 0.62 / 2.23 / 8.01 / 7.67 -- the product default where its limits allow.
 #include "mtq_awq_w4.inc"
 
 template <typename T, bool HAS_BIAS>
@@ -432,7 +431,7 @@ __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
   const unsigned wb0 = lds0 + 32768 + wn * 16384 + lt0, wb1 = lds0 + 32768 + wn * 16384 + lt1;
   const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + wave * 8192);
   const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
-  unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)(K / 64 - 2));
+  unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 2) / 2));  // two tiles per pass
   // reference-tile DMA sources: half h (rows 128 h ..) lands in slot (K / 64 + h) % 2; wave w
   // fills rows 32 w + 2 u + (l >> 5), u = 0..15, row r's 16-byte chunk c at c ^ (r & 15)
   const unsigned yrb = __builtin_amdgcn_readfirstlane((unsigned)(((m0 + 32 * wave) * p.N + n0) * 2));
@@ -661,9 +660,9 @@ extern "C" int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const
   // 32 slots per 8 x 4 tile unit, units padded to a multiple of the 8 XCDs (see the kernel)
   const int64_t units = (int64_t)G * ((tiles_m + 7) / 8) * ((tiles_n + 3) / 4);
   const dim3 grid((unsigned)((units + 7) / 8 * 8 * 32));
-  const bool w4_ok = K >= 128 && M * N * 2 < ((int64_t)1 << 32);
+  const bool w4_ok = K >= 128 && K % 128 == 0 && M * N * 2 < ((int64_t)1 << 32);
   if (kernel == MTQ_AWQ_SEARCH_W4 && !w4_ok) return MTQ_ERR_INVALID_ARG;
-  if (kernel == MTQ_AWQ_SEARCH_W4) {
+  if (kernel == MTQ_AWQ_SEARCH_W4 || (kernel == MTQ_AWQ_SEARCH_AUTO && w4_ok)) {
     count_dispatch(kDispAwqSearchW4);
     if (dtype == MTQ_BF16) {
       if (bias)

@@ -423,8 +423,11 @@ def _mse_fast(out, ref) -> bool:
 
 
 # Fused AWQ search on MFMA (csrc/mtq_awq_gemm.hip): used for linears with at most this many output
-# features, where it beats the library path (k/v_proj, scripts/bench_awq_gemm.py); wider linears run
-# one hipBLASLt GEMM per alpha between one x * (1/s) pass and one loss pass for all alphas.
+# features or with at least as many output as input features, where it beats the library path
+# (r06, the one-wave-per-SIMD kernel, scripts/bench_awq_gemm.py at Llama-3-8B shapes: k/v, q/o,
+# gate/up fused; down_proj -- K 14336 > N 4096, whose x * (1/s) pass alone is 0.6 ms of the fused
+# call -- keeps the library); the others run one hipBLASLt GEMM per alpha between one x * (1/s)
+# pass and one loss pass for all alphas.
 # MTQ_AMD_AWQ_FUSED: "auto" (default), "always" (fused kernel for every width), "library" (the
 # hipBLASLt path for every width), "never" (the reference's per-alpha loop, no fast path).
 _AWQ_FUSED_MAX_N = 2048
@@ -497,7 +500,8 @@ def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
     # the fused kernel's limits (mtq_awq_search_gemm: G <= 64, 32-bit element offsets); the
     # batched path's loss pass takes G <= 16; anything else runs one alpha at a time
     fused_ok = n_alpha <= _AWQ_FUSED_MAX_G and x2.shape[0] * k_in < 2**31 and n_out * k_in < 2**31
-    fused = fused_ok and (_AWQ_FUSED == "always" or (_AWQ_FUSED == "auto" and n_out <= _AWQ_FUSED_MAX_N))
+    fused = fused_ok and (_AWQ_FUSED == "always" or
+                          (_AWQ_FUSED == "auto" and (n_out <= _AWQ_FUSED_MAX_N or k_in <= n_out)))
     if fused:
         ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
     elif n_alpha <= 16:

@@ -15,8 +15,7 @@ without storing the GEMM output.  Checks:
 * the weight side ``block_quant_dynamic_multi`` equals G single-alpha launches bit for bit.
 Both search kernels run every check: ``kernel=1`` the r03 ping-pong kernel (8 waves), ``kernel=2``
 the r06 one-wave-per-SIMD kernel whose K loop is generated inline asm (scripts/gen_awq_w4.py; K >=
-128); ``kernel=0`` (what the product calls) is the first, the faster one at the widths the fused
-search serves.
+128, K % 128 == 0); ``kernel=0`` (what the product calls) is the second where its limits allow.
 """
 
 import pytest
@@ -54,8 +53,8 @@ def _host_loss(x, sinv, wq, bias, yref):
 @pytest.mark.parametrize("with_bias", [False, True])
 def test_exact_integer_data(gpu, dtype, shape, with_bias, kernel):
     M, N, K = shape
-    if kernel == 2 and K < 128:
-        pytest.skip("the W4 kernel needs K >= 128 (test_kernel_choice covers the rejection)")
+    if kernel == 2 and K % 128:
+        pytest.skip("the W4 kernel needs K % 128 == 0 (test_kernel_choice covers the rejection)")
     G = 3
     g = torch.Generator().manual_seed(M + N + K)
     # sparse small integers: every product sum, output, difference and square sum (per lane,
@@ -110,13 +109,13 @@ def test_llama_shapes_vs_unfused(gpu, nk, kernel):
 
 
 def test_kernel_choice(gpu):
-    """kernel=0 (the product call) runs the ping-pong kernel, kernel=2 the W4 kernel; asking for W4
-    at K = 64 is an error, not a silent fallback."""
+    """kernel=0 (the product call) runs the W4 kernel where K % 128 == 0 and the ping-pong kernel
+    otherwise; asking for W4 at K = 64 is an error, not a silent fallback."""
     from modelopt_amd import _ext as ext
 
     dt = torch.bfloat16
-    for K, kernel, want in ((64, 0, "awq_search_pp"), (4096, 0, "awq_search_pp"), (128, 2, "awq_search_w4"),
-                            (4096, 2, "awq_search_w4"), (4096, 1, "awq_search_pp")):
+    for K, kernel, want in ((64, 0, "awq_search_pp"), (192, 0, "awq_search_pp"), (4096, 0, "awq_search_w4"),
+                            (128, 2, "awq_search_w4"), (4096, 1, "awq_search_pp")):
         x = torch.randn(256, K, device=gpu).to(dt)
         wq = torch.randn(2, 256, K, device=gpu).to(dt)
         sinv = torch.ones(2, K, device=gpu, dtype=dt)

@@ -6,9 +6,9 @@ kernels the bench and C2 / C3 run are the ones compared end to end:
 
 * a 2-layer Llama (hidden 4096, intermediate 14336, 32 / 8 heads, bf16) under FP8_DEFAULT_CFG
   (per-tensor amax: ``amax_persist``), INT8_DEFAULT_CFG (per-channel weights: ``amax_rows_u``,
-  ``ew_rowwave``) and INT4_AWQ_CFG (awq_lite, block 128: the fused ``awq_search_pp`` search on
-  k/v (N = 1024), the batched library path on q/o/gate/up/down, ``ew_group_sk`` for the promoted
-  static-block weights);
+  ``ew_rowwave``) and INT4_AWQ_CFG (awq_lite, block 128: the fused ``awq_search_w4`` search on
+  k/v/q/o/gate/up, the batched library path on down, ``ew_group_sk`` for the promoted static-block
+  weights);
 * a Mixtral layer at hidden 1024 with 8 experts (the fused-experts plugin) under FP8_DEFAULT_CFG.
 
 The weights are regenerated from the seed (``tests/golden/prod_models.py``) and checked against the
@@ -50,7 +50,7 @@ from prod_models import PROD_CASES, fingerprint, prod_inputs, prod_model, sha  #
 EXPECTED_KERNELS = {
     "llama_fp8": ["amax_persist", "ew_vec"],
     "llama_int8": ["amax_persist", "amax_rows_u", "ew_rowwave"],
-    "llama_int4_awq": ["awq_search_pp", "awq_prescale", "awq_mse_multi", "block_quant_dyn", "ew_group_sk"],
+    "llama_int4_awq": ["awq_search_w4", "awq_prescale", "awq_mse_multi", "block_quant_dyn", "ew_group_sk"],
     "mixtral_fp8": ["amax_persist", "ew_vec"],
 }
 
