@@ -26,6 +26,8 @@ w4.awq_w4asm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.
 VARS = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "31,34,35,50,53".split(","))]
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 SHAPES = {"k_proj": (1024, 4096), "q_proj": (4096, 4096), "gate_proj": (14336, 4096), "down_proj": (4096, 14336)}
+if len(sys.argv) > 3:  # e.g. "q_proj=4096x4096,q_k2=4096x8192"
+    SHAPES = {kv.split("=")[0]: tuple(int(v) for v in kv.split("=")[1].split("x")) for kv in sys.argv[3].split(",")}
 M, G = 8192, 11
 dev = torch.device("cuda")
 stream = torch.cuda.current_stream().cuda_stream

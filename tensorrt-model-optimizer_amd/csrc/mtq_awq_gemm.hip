@@ -382,6 +382,9 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
 // the pp kernel's 0.62 / 2.23 / 8.01 / 7.67 -- the product default where its limits allow.
 #include "mtq_awq_w4.inc"
 
+typedef float w4f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 w4b2 __attribute__((ext_vector_type(2)));
+
 template <typename T, bool HAS_BIAS>
 __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[131072];
@@ -479,6 +482,11 @@ __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
   }
   float sum = 0.f;
   float o[32];
+  // a whole tile inside the matrix (uniform): no masks; for bf16 the output / difference pairs
+  // rounded by one v_cvt_pk_bf16_f32 each and squared-summed by v_dot2c_f32_bf16 (exact
+  // products; 4 per element instead of 9 VALU instructions -- the epilogue was ~8 % of a
+  // K = 4096 tile, profiles/r06/awq/)
+  const bool full = m0 + kBM <= p.M && n0 + kBN <= p.N;
 #define MTQ_W4_EPI(I)                                                                                 \
   {                                                                                                   \
     MTQ_W4_STRIP_##I(o);                                                                              \
@@ -490,14 +498,46 @@ __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
       __builtin_memcpy(yv, lds + yslot + rr * 512 + (((cl >> 3) ^ fr) << 4) + (cl & 7) * 2, 8);       \
       const bool ok = rok && cok[j];                                                                  \
       _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                 \
-        const float y = Elem<T>::ld(Elem<T>::st(o[4 * j + e] + bj[j][e]));                            \
+        const float y = Elem<T>::ld(Elem<T>::st(HAS_BIAS ? o[4 * j + e] + bj[j][e] : o[4 * j + e]));  \
         const float d = Elem<T>::ld(Elem<T>::st(y - Elem<T>::ld(yv[e])));                             \
         sum = ok ? __builtin_fmaf(d, d, sum) : sum;                                                   \
       }                                                                                               \
     }                                                                                                 \
   }
-  MTQ_W4_EPI(0) MTQ_W4_EPI(1) MTQ_W4_EPI(2) MTQ_W4_EPI(3) MTQ_W4_EPI(4) MTQ_W4_EPI(5) MTQ_W4_EPI(6) MTQ_W4_EPI(7)
+#define MTQ_W4_EPI_BF16(I)                                                                            \
+  {                                                                                                   \
+    MTQ_W4_STRIP_##I(o);                                                                              \
+    const int rr = 16 * (I) + fr;                                                                     \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                   \
+      const int cl = wn * 128 + 16 * j + 4 * fq;                                                      \
+      uint32_t yr[2];                                                                                 \
+      __builtin_memcpy(yr, lds + yslot + rr * 512 + (((cl >> 3) ^ fr) << 4) + (cl & 7) * 2, 8);       \
+      _Pragma("unroll") for (int h = 0; h < 2; ++h) {                                                 \
+        w4f2 y = {o[4 * j + 2 * h], o[4 * j + 2 * h + 1]};                                            \
+        if (HAS_BIAS) y += w4f2{bj[j][2 * h], bj[j][2 * h + 1]};                                     \
+        const uint32_t yu = __builtin_bit_cast(uint32_t, __builtin_convertvector(y, w4b2));           \
+        const w4f2 yf = {__builtin_bit_cast(float, yu << 16), __builtin_bit_cast(float, yu & 0xffff0000u)}; \
+        const w4f2 rf = {__builtin_bit_cast(float, yr[h] << 16),                                      \
+                         __builtin_bit_cast(float, yr[h] & 0xffff0000u)};                             \
+        const w4b2 d = __builtin_convertvector(yf - rf, w4b2);                                        \
+        s4[(2 * j + h) & 3] = __builtin_amdgcn_fdot2_f32_bf16(d, d, s4[(2 * j + h) & 3], false);      \
+      }                                                                                               \
+    }                                                                                                 \
+  }
+  if constexpr (__is_same(T, __bf16)) {
+    if (full) {
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      MTQ_W4_EPI_BF16(0) MTQ_W4_EPI_BF16(1) MTQ_W4_EPI_BF16(2) MTQ_W4_EPI_BF16(3)
+      MTQ_W4_EPI_BF16(4) MTQ_W4_EPI_BF16(5) MTQ_W4_EPI_BF16(6) MTQ_W4_EPI_BF16(7)
+      sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    } else {
+      MTQ_W4_EPI(0) MTQ_W4_EPI(1) MTQ_W4_EPI(2) MTQ_W4_EPI(3) MTQ_W4_EPI(4) MTQ_W4_EPI(5) MTQ_W4_EPI(6) MTQ_W4_EPI(7)
+    }
+  } else {
+    MTQ_W4_EPI(0) MTQ_W4_EPI(1) MTQ_W4_EPI(2) MTQ_W4_EPI(3) MTQ_W4_EPI(4) MTQ_W4_EPI(5) MTQ_W4_EPI(6) MTQ_W4_EPI(7)
+  }
 #undef MTQ_W4_EPI
+#undef MTQ_W4_EPI_BF16
   __syncthreads();
 #pragma unroll
   for (int o2 = 32; o2 >= 1; o2 >>= 1) sum += __shfl_xor(sum, o2);
