@@ -14,6 +14,9 @@ Also reported (same JSON line):
   roofline      dominant kernel: algorithmic bytes per launch / mean launch time (HIP events on
                 the launch stream) vs 8.0 TB/s; `traffic` from the PMC profile in profiles/ if present
   kernels       per-kernel G-elem/s and % roofline for the other hot-path formats
+  attention_p_qdq  the fused flash attention with softmax-P qdq, MFMA TFLOP/s per P mode
+  awq_search    the AWQ-lite alpha search of one calibration batch on q_proj / gate_proj shapes:
+                fused MFMA search call vs the batched hipBLASLt path it replaces (TFLOP/s, % peak)
   cpu_baseline  the oracle's restatement of the reference eager path (tensor_quant.py:46-59) timed
                 on this host's cores on a bounded sample (rank 0, N=1 only)
   ptq           Llama-3-8B FP8 PTQ wall-clock (512 synthetic samples x 512 tokens; DP over ranks,
@@ -272,6 +275,69 @@ def attention_suite(iters: int = 50):
     return r
 
 
+def awq_search_suite(rounds: int = 3):
+    """N1: the AWQ-lite alpha search of one calibration batch (8192 tokens, 11 alphas) on
+    Llama-3-8B's q_proj and gate_proj shapes -- the fused call (x * (1/s) pass + the W4 MFMA
+    search kernel with the loss in its epilogue, mtq_awq_search_gemm) beside the batched path it
+    replaces (the same pass + 11 hipBLASLt GEMMs + one loss pass) and the 11 GEMMs alone; MFMA
+    TFLOP/s = 2 M N K G / time against the 2.5 PF dense bf16 peak.  Interleaved rounds, medians."""
+    import statistics  # noqa: PLC0415
+
+    import torch.nn.functional as F  # noqa: PLC0415
+
+    from modelopt_amd import _ext  # noqa: PLC0415
+
+    ops = _ext.ops()
+    M, G, res = 8192, 11, {}
+    for name, (N, K) in {"q_proj": (4096, 4096), "gate_proj": (14336, 4096)}.items():
+        gen = torch.Generator(device="cuda").manual_seed(N + K)
+        x = torch.randn(M, K, device="cuda", generator=gen).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda", generator=gen) * 0.02).to(torch.bfloat16)
+        s = torch.rand(G, K, device="cuda", generator=gen) * 3 + 0.25
+        si = (1 / s).to(torch.bfloat16)
+        wq = ops.block_quant_dynamic_multi(w, s.to(torch.bfloat16), 128, 4, False, False)
+        yref = F.linear(x, w)
+        loss = torch.zeros(G, device="cuda")
+        out = torch.empty((G, M, N), dtype=x.dtype, device="cuda")
+
+        def fused():
+            ops.awq_search_gemm(x, si, wq, None, yref, loss)
+
+        def batched():
+            xs = ops.awq_prescale(x, si)
+            for g in range(G):
+                torch.mm(xs[g], wq[g].t(), out=out[g])
+            ops.awq_mse_multi(out, yref, loss)
+
+        def gemms():
+            for g in range(G):
+                torch.mm(x, wq[g].t(), out=out[g])
+
+        arms = {"fused_search": fused, "batched_hipblaslt_path": batched, "hipblaslt_gemms_alone": gemms}
+        t = {k: [] for k in arms}
+        for _ in range(rounds):
+            for k, f in arms.items():
+                f()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    f()
+                e1.record()
+                torch.cuda.synchronize()
+                t[k].append(e0.elapsed_time(e1) / 3)
+        flop = 2.0 * M * N * K * G
+        r = {k: {"ms": round(statistics.median(v), 3),
+                 "tflops": round(flop / (statistics.median(v) * 1e-3) / 1e12, 1)} for k, v in t.items()}
+        for v in r.values():
+            v["frac_mfma_peak"] = round(v["tflops"] / 2500.0, 4)
+        r["fused_speedup_vs_batched"] = round(r["batched_hipblaslt_path"]["ms"] / r["fused_search"]["ms"], 3)
+        res[name] = r
+        del x, w, wq, yref, out
+    torch.cuda.empty_cache()
+    return {"tokens": M, "alphas": G, "dtype": "bf16", "shapes": res}
+
+
 def host_cpu_info():
     """Physical cores of the host (unique (package, core) pairs in /proc/cpuinfo), the CPUs this
     process may run on, and torch's intra-op thread count."""
@@ -514,6 +580,7 @@ def main():
     if rank == 0 and not args.no_suite:
         out["kernels"] = kernel_suite(ops, xs, args.steps, args.warmup)
         out["attention_p_qdq"] = attention_suite()
+        out["awq_search"] = awq_search_suite()
     if not args.no_ptq:
         from benchmarks import ptq_llama  # noqa: PLC0415
 
