@@ -111,14 +111,15 @@ def tile(op, k1set, yhalf=None):
 
 def body(op):
     L = ["s_nop 4"]  # SGPR inputs fresh from v_readfirstlane, read by buffer instructions
-    L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
     L += ["s_mov_b32 %[koff], 0", "s_mov_b32 %[sdma], 0"]
     for t in range(2):
         L += ["s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128",
               f"s_add_u32 %[m0s], %[m0b], {t * 65536}"]
         for d in kdmas():
             L += d
-    L += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    # the accumulators zeroed while the first two tiles are in flight
+    L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
+    L += ["s_nop 2", "s_waitcnt vmcnt(16)", "s_barrier"]
     L += reads(0, "%[xb0]", "%[wb0]") + reads(1, "%[xb1]", "%[wb1]")
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]  # slot 0 free for tile 2's DMAs
     L += ["s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_tail_%="]  # K = 128: the two peeled tiles only
