@@ -94,13 +94,13 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
-      unsigned m0y, yso;
+      unsigned m0y, yso, ybs;
       // EPI 3 (T64B): the loop runs two tiles per pass (K % 128 == 0)
       unsigned cnt2 = __builtin_amdgcn_readfirstlane((unsigned)(EPI == 3 ? (K / 64 - 2) / 2 : K / 64 - 2));
 #define W4_ASMY(BODY) \
       asm volatile(BODY \
                    : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
-                     [cnt] "+s"(cnt2), [m0y] "=&s"(m0y), [yso] "=&s"(yso) \
+                     [cnt] "+s"(cnt2), [m0y] "=&s"(m0y), [yso] "=&s"(yso), [ybs] "=&s"(ybs) \
                    : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast), \
                      [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]), \
                      [xo4] "v"(xo[4]), [xo5] "v"(xo[5]), [xo6] "v"(xo[6]), [xo7] "v"(xo[7]), \
@@ -115,8 +115,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
       if constexpr (V == 1) W4_ASMY(W4ASM_BODY_Y_1);
       if constexpr (V == 2) W4_ASMY(W4ASM_BODY_Y_2);
       if constexpr (V == 3) W4_ASMY(W4ASM_BODY_Y_3);
-      if constexpr (V == 4) W4_ASMY(W4ASM_BODY_Y_4);
-      if constexpr (V == 5) W4_ASMY(W4ASM_BODY_Y_5);
+
 
 #undef W4_ASMY
     }
@@ -196,8 +195,6 @@ extern "C" int awq_w4asm(int var, const void *xs, const void *wq, const void *yr
   case 1: return go<1>(a, stream);
   case 2: return go<2>(a, stream);
   case 3: return go<3>(a, stream);
-  case 4: return go<4>(a, stream);
-  case 5: return go<5>(a, stream);
   default: return 3;
   }
 }

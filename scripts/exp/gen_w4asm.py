@@ -33,12 +33,10 @@ SLOT = 32768
 # EPI 2: the reference tile prefetched into the LDS ring by the last two K tiles (body_t64y)
 # EPI 3: T64B (three fragment sets, two barriers per tile, DMAs two tiles ahead from the tile start)
 VARIANTS = [
-    (2, "spread/spread/0", 2, 0, 1, "", 3, 8),
     (2, "front/spread/0", 2, 0, 1, "", 3, 8),
-    (2, "spread/front/0", 2, 0, 1, "", 3, 8),
-    (2, "front/front/0", 2, 0, 1, "", 3, 8),
-    (2, "spread/spread/1", 2, 0, 1, "", 3, 8),
-    (2, "spread/spread/2", 2, 0, 1, "", 3, 8),
+    (2, "front/split/0", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0", 2, 0, 1, "", 3, 8),
+    (2, "front/splitmix/0", 2, 0, 1, "", 3, 8),
 ]
 CACHE = ""
 
@@ -180,13 +178,13 @@ def reads64(s, xb, wb):
 
 def ydmas():
     """16 LDS-DMAs of one 128-row half of the reference (yref) tile into the current slot: wave w
-    fills rows 32 w + 2 u + (l >> 5) (512 B each), u = 0..15; the row advance in the scalar
-    offset %[yso] (+ %[ys2] = two rows per DMA), the lane's XOR-swizzled chunk in yo(u % 8)."""
+    fills rows 32 w + 2 u + (l >> 5) (512 B each), u = 0..15; each DMA's scalar offset computed
+    from the half's base %[ybs] (any issue order), the lane's XOR-swizzled chunk in yo(u % 8)."""
     out = []
     for u in range(16):
-        out.append([f"s_add_u32 m0, %[m0y], {u * 1024}", "s_nop 0",
-                    f"buffer_load_dwordx4 %[yo{u % 8}], %[yr], %[yso] offen lds",
-                    "s_add_u32 %[yso], %[yso], %[ys2]"])
+        out.append([f"s_add_u32 m0, %[m0y], {u * 1024}", f"s_mul_i32 %[yso], %[ys2], {u}",
+                    "s_add_u32 %[yso], %[yso], %[ybs]",
+                    f"buffer_load_dwordx4 %[yo{u % 8}], %[yr], %[yso] offen lds"])
     return out
 
 
@@ -291,13 +289,18 @@ def reads3(s, xb, wb):
 B3_READS = "spread"   # "spread": one per 2 MFMAs; "front": one per MFMA over the first 32
 B3_DMAS = "spread"    # "spread": one per 4 MFMAs; "front": one per 2 over the first 32
 B3_PROBE = 0          # 1: no K-tile DMAs in the loop; 2: they re-load tile 0 (L2 hits)
+# "split*": 8 DMAs in phase 1, 8 in phase 2's second half; the order of dm indices (X = 0..7, W = 8..15)
+# (each DMA group of 4 must keep its M0 write first: dm[0] / dm[4] / dm[8] / dm[12] carry it)
+SPLIT_ORDER = {"split": list(range(16)),
+               "splitwx": list(range(8, 16)) + list(range(8)),
+               "splitmix": [0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15]}
 
 
 def tile3(k1set, yhalf=None):
     nk1 = 3 - k1set  # the next tile's k-half-1 set (B <-> C)
     L = ["s_add_u32 %[m0s], %[m0b], %[sdma]"] if yhalf is None else \
         ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
-         "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
+         "s_mov_b32 %[ybs], %[yrb]" if yhalf == 0 else "s_add_u32 %[ybs], %[yrb], %[yh]"]
     if yhalf is None:
         L += ["s_min_u32 %[kc], %[koff], %[klast]" if B3_PROBE != 2 else "s_mov_b32 %[kc], 0",
               "s_add_u32 %[koff], %[koff], 128"]
@@ -310,7 +313,9 @@ def tile3(k1set, yhalf=None):
             L += dm[n // 4]
         if B3_DMAS == "front" and n < 32 and n % 2 == 0:
             L += dm[n // 2]
-    L += ["s_waitcnt vmcnt(16)", "s_barrier",
+        if B3_DMAS.startswith("split") and n % 8 == 1:
+            L += dm[SPLIT_ORDER[B3_DMAS][n // 8]]
+    L += ["s_waitcnt vmcnt(16)" if not B3_DMAS.startswith("split") else "s_waitcnt vmcnt(8)", "s_barrier",
           "s_xor_b32 %[srd], %[sdma], 65536",
           "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
           "v_add_u32 v62, %[srd], %[xb1]", "v_add_u32 v63, %[srd], %[wb1]"]
@@ -321,6 +326,8 @@ def tile3(k1set, yhalf=None):
             L.append(rd[n // 2])
         if B3_READS == "front" and n < 32:
             L.append(rd[n])
+        if B3_DMAS.startswith("split") and n >= 33 and (n - 33) % 4 == 0 and (n - 33) // 4 < 8:
+            L += dm[SPLIT_ORDER[B3_DMAS][8 + (n - 33) // 4]]
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
     return L
 

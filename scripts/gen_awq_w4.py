@@ -16,10 +16,12 @@ hipcc's waits collapse its prefetch; DESIGN.md §4e, measured in scripts/exp/awq
   tile's second phase, so its LDS slot is free from that tile's end and the DMAs two tiles ahead
   get three MFMA phases to land (a two-set schedule freed the slot one phase later and gave them
   one and a half: 5-9 % slower, scripts/exp/gen_w4asm.py);
-* per tile t: phase 1 = 64 MFMAs on A (k0 of t) with the 16 DMAs of tile t+2 into slot t % 2
-  (one per 4 MFMAs); vmcnt(16) (this wave's DMAs of tile t+1 landed) + s_barrier; phase 2 = 64
-  MFMAs on B|C (k1 of t) with the 32 ds_read_b128 of tile t+1 (k0 -> A, k1 -> the other of B|C)
-  one per MFMA over the first 32; lgkmcnt(0) + s_barrier.  Every wait counted by hand;
+* per tile t: phase 1 = 64 MFMAs on A (k0 of t) with the 8 W-part DMAs of tile t+2 into slot
+  t % 2 (one per 8 MFMAs); vmcnt(8) (this wave's DMAs of tile t+1 landed) + s_barrier; phase 2 =
+  64 MFMAs on B|C (k1 of t) with the 32 ds_read_b128 of tile t+1 (k0 -> A, k1 -> the other of
+  B|C) one per MFMA over the first 32, then the 8 X-part DMAs of tile t+2 over the second 32
+  (away from the reads; W first: 0.3-5 % faster than all 16 in phase 1, X-first split slower on
+  gate, scripts/exp/gen_w4asm.py "splitwx"); lgkmcnt(0) + s_barrier.  Every wait counted by hand;
 * the last two tiles are peeled: their DMA slots carry the epilogue's reference (yref) tile, half
   h (rows 128 h ..) into slot (K / 64 + h) % 2 with the 16-byte chunk c of row r at c ^ (r & 15),
   so the epilogue reads it from LDS without a load round trip.
@@ -31,8 +33,10 @@ from pathlib import Path
 OUT = Path(__file__).resolve().parents[1] / "tensorrt-model-optimizer_amd" / "csrc" / "mtq_awq_w4.inc"
 SET_BASE = (64, 128, 192)  # A, B, C
 MFMA = {"BF16": "v_mfma_f32_16x16x32_bf16", "F16": "v_mfma_f32_16x16x32_f16"}
-# placement (after MFMA #): phase-1 DMAs of tile t+2, phase-2 reads of tile t+1
-P1_DMAS = [4 * k + 1 for k in range(16)]
+# placement (after MFMA #): phase-1 DMAs (the W part) and phase-2 DMAs (the X part) of tile t+2,
+# phase-2 reads of tile t+1
+P1_DMAS = [8 * k + 1 for k in range(8)]
+P2_DMAS = [33 + 4 * k for k in range(8)]
 P2_READS = list(range(32))
 
 
@@ -74,12 +78,13 @@ def kdmas():
 
 def ydmas():
     """16 DMAs of one 128-row half of the yref tile: wave w fills rows 32 w + 2 u + (l >> 5) (512 B
-    each); the row advance in the scalar offset, the lane's swizzled chunk in yo(u % 8)."""
+    each); each DMA's scalar offset = the half's base %[ybs] + u rows pairs (any issue order), the
+    lane's swizzled chunk in yo(u % 8)."""
     out = []
     for u in range(16):
-        out.append([f"s_add_u32 m0, %[m0y], {u * 1024}", "s_nop 0",
-                    f"buffer_load_dwordx4 %[yo{u % 8}], %[yr], %[yso] offen lds",
-                    "s_add_u32 %[yso], %[yso], %[ys2]"])
+        out.append([f"s_add_u32 m0, %[m0y], {u * 1024}", f"s_mul_i32 %[yso], %[ys2], {u}",
+                    "s_add_u32 %[yso], %[yso], %[ybs]",
+                    f"buffer_load_dwordx4 %[yo{u % 8}], %[yr], %[yso] offen lds"])
     return out
 
 
@@ -91,13 +96,14 @@ def tile(op, k1set, yhalf=None):
         dm = kdmas()
     else:
         L = ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
-             "s_mov_b32 %[yso], %[yrb]" if yhalf == 0 else "s_add_u32 %[yso], %[yrb], %[yh]"]
+             "s_mov_b32 %[ybs], %[yrb]" if yhalf == 0 else "s_add_u32 %[ybs], %[yrb], %[yh]"]
         dm = ydmas()
+    dm = dm[8:] + dm[:8]  # the W part (or the yref half's second 8 rows pairs) first
     for n in range(64):
         L.append(mfma(op, 0, n // 8, n % 8))
         if n in P1_DMAS:
             L += dm[P1_DMAS.index(n)]
-    L += ["s_waitcnt vmcnt(16)", "s_barrier", "s_xor_b32 %[srd], %[sdma], 65536",
+    L += ["s_waitcnt vmcnt(8)", "s_barrier", "s_xor_b32 %[srd], %[sdma], 65536",
           "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
           "v_add_u32 v62, %[srd], %[xb1]", "v_add_u32 v63, %[srd], %[wb1]"]
     rd = reads(0, "v60", "v61") + reads(3 - k1set, "v62", "v63")
@@ -105,6 +111,8 @@ def tile(op, k1set, yhalf=None):
         L.append(mfma(op, k1set, n // 8, n % 8))
         if n in P2_READS:
             L.append(rd[P2_READS.index(n)])
+        if n in P2_DMAS:
+            L += dm[8 + P2_DMAS.index(n)]
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
     return L
 

@@ -445,11 +445,11 @@ __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
 #pragma unroll
   for (int k = 0; k < 8; ++k)
     yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
-  unsigned koff, kc, m0s, sdma, srd, m0y, yso;
+  unsigned koff, kc, m0s, sdma, srd, m0y, yso, ybs;
 #define MTQ_W4_ASM(BODY)                                                                              \
   asm volatile(BODY                                                                                   \
                : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
-                 [cnt] "+s"(cnt), [m0y] "=&s"(m0y), [yso] "=&s"(yso)                                     \
+                 [cnt] "+s"(cnt), [m0y] "=&s"(m0y), [yso] "=&s"(yso), [ybs] "=&s"(ybs)                 \
                : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast),                         \
                  [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]),                  \
                  [xo4] "v"(xo[4]), [xo5] "v"(xo[5]), [xo6] "v"(xo[6]), [xo7] "v"(xo[7]),                  \
