@@ -33,10 +33,11 @@ SLOT = 32768
 # EPI 2: the reference tile prefetched into the LDS ring by the last two K tiles (body_t64y)
 # EPI 3: T64B (three fragment sets, two barriers per tile, DMAs two tiles ahead from the tile start)
 VARIANTS = [
-    (2, "front/spread/0", 2, 0, 1, "", 3, 8),
-    (2, "front/split/0", 2, 0, 1, "", 3, 8),
-    (2, "front/splitwx/0", 2, 0, 1, "", 3, 8),
-    (2, "front/splitmix/0", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0/a", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0/b", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0/c", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0/d", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0/e", 2, 0, 1, "", 3, 8),
 ]
 CACHE = ""
 
@@ -291,6 +292,11 @@ B3_DMAS = "spread"    # "spread": one per 4 MFMAs; "front": one per 2 over the f
 B3_PROBE = 0          # 1: no K-tile DMAs in the loop; 2: they re-load tile 0 (L2 hits)
 # "split*": 8 DMAs in phase 1, 8 in phase 2's second half; the order of dm indices (X = 0..7, W = 8..15)
 # (each DMA group of 4 must keep its M0 write first: dm[0] / dm[4] / dm[8] / dm[12] carry it)
+B3_POS = "a"
+P1POS = {"a": [8 * k + 1 for k in range(8)], "b": [2 * k + 1 for k in range(8)], "c": [8 * k + 1 for k in range(8)],
+         "d": [8 * k + 5 for k in range(8)], "e": [4 * k + 1 for k in range(8)]}
+P2POS = {"a": [33 + 4 * k for k in range(8)], "b": [33 + 4 * k for k in range(8)], "c": [32 + 2 * k for k in range(8)],
+         "d": [35 + 4 * k for k in range(8)], "e": [33 + 4 * k for k in range(8)]}
 SPLIT_ORDER = {"split": list(range(16)),
                "splitwx": list(range(8, 16)) + list(range(8)),
                "splitmix": [0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15]}
@@ -313,8 +319,8 @@ def tile3(k1set, yhalf=None):
             L += dm[n // 4]
         if B3_DMAS == "front" and n < 32 and n % 2 == 0:
             L += dm[n // 2]
-        if B3_DMAS.startswith("split") and n % 8 == 1:
-            L += dm[SPLIT_ORDER[B3_DMAS][n // 8]]
+        if B3_DMAS.startswith("split") and n in P1POS[B3_POS]:
+            L += dm[SPLIT_ORDER[B3_DMAS][P1POS[B3_POS].index(n)]]
     L += ["s_waitcnt vmcnt(16)" if not B3_DMAS.startswith("split") else "s_waitcnt vmcnt(8)", "s_barrier",
           "s_xor_b32 %[srd], %[sdma], 65536",
           "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
@@ -326,8 +332,8 @@ def tile3(k1set, yhalf=None):
             L.append(rd[n // 2])
         if B3_READS == "front" and n < 32:
             L.append(rd[n])
-        if B3_DMAS.startswith("split") and n >= 33 and (n - 33) % 4 == 0 and (n - 33) // 4 < 8:
-            L += dm[SPLIT_ORDER[B3_DMAS][8 + (n - 33) // 4]]
+        if B3_DMAS.startswith("split") and n in P2POS[B3_POS]:
+            L += dm[SPLIT_ORDER[B3_DMAS][8 + P2POS[B3_POS].index(n)]]
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
     return L
 
@@ -413,7 +419,9 @@ def main():
     for v, (S, order, swz, probe, ofs, CACHE, _epi, _gm) in enumerate(VARIANTS):
         if S == 2 and _epi == 3:
             global B3_READS, B3_DMAS, B3_PROBE
-            B3_READS, B3_DMAS, pr = order.split("/")
+            global B3_POS
+            B3_READS, B3_DMAS, pr = order.split("/")[:3]
+            B3_POS = order.split("/")[3] if order.count("/") >= 3 else "a"
             B3_PROBE = int(pr)
             lines = body_t64b()
         elif S == 2:
