@@ -34,10 +34,8 @@ SLOT = 32768
 # EPI 3: T64B (three fragment sets, two barriers per tile, DMAs two tiles ahead from the tile start)
 VARIANTS = [
     (2, "front/splitwx/0/a", 2, 0, 1, "", 3, 8),
-    (2, "front/splitwx/0/b", 2, 0, 1, "", 3, 8),
-    (2, "front/splitwx/0/c", 2, 0, 1, "", 3, 8),
-    (2, "front/splitwx/0/d", 2, 0, 1, "", 3, 8),
-    (2, "front/splitwx/0/e", 2, 0, 1, "", 3, 8),
+    (2, "win40/splitwx/0/f", 2, 0, 1, "", 3, 8),
+    (2, "win48/splitwx/0/g", 2, 0, 1, "", 3, 8),
 ]
 CACHE = ""
 
@@ -293,9 +291,10 @@ B3_PROBE = 0          # 1: no K-tile DMAs in the loop; 2: they re-load tile 0 (L
 # "split*": 8 DMAs in phase 1, 8 in phase 2's second half; the order of dm indices (X = 0..7, W = 8..15)
 # (each DMA group of 4 must keep its M0 write first: dm[0] / dm[4] / dm[8] / dm[12] carry it)
 B3_POS = "a"
-P1POS = {"a": [8 * k + 1 for k in range(8)], "b": [2 * k + 1 for k in range(8)], "c": [8 * k + 1 for k in range(8)],
+RWIN = {"win40": [int(k * 40 / 32) for k in range(32)], "win48": [int(k * 48 / 32) for k in range(32)]}
+P1POS = {"f": [8 * k + 1 for k in range(8)], "g": [8 * k + 1 for k in range(8)], "a": [8 * k + 1 for k in range(8)], "b": [2 * k + 1 for k in range(8)], "c": [8 * k + 1 for k in range(8)],
          "d": [8 * k + 5 for k in range(8)], "e": [4 * k + 1 for k in range(8)]}
-P2POS = {"a": [33 + 4 * k for k in range(8)], "b": [33 + 4 * k for k in range(8)], "c": [32 + 2 * k for k in range(8)],
+P2POS = {"f": [41 + 2 * k + (k // 2) for k in range(8)], "g": [49 + 2 * k for k in range(8)], "a": [33 + 4 * k for k in range(8)], "b": [33 + 4 * k for k in range(8)], "c": [32 + 2 * k for k in range(8)],
          "d": [35 + 4 * k for k in range(8)], "e": [33 + 4 * k for k in range(8)]}
 SPLIT_ORDER = {"split": list(range(16)),
                "splitwx": list(range(8, 16)) + list(range(8)),
@@ -332,6 +331,10 @@ def tile3(k1set, yhalf=None):
             L.append(rd[n // 2])
         if B3_READS == "front" and n < 32:
             L.append(rd[n])
+        if B3_READS.startswith("win"):  # a window of >= 32 MFMAs: at most one read per position
+            for k, at in enumerate(RWIN[B3_READS]):
+                if at == n:
+                    L.append(rd[k])
         if B3_DMAS.startswith("split") and n in P2POS[B3_POS]:
             L += dm[SPLIT_ORDER[B3_DMAS][8 + P2POS[B3_POS].index(n)]]
     L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
