@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
       if constexpr (V == 0) W4_ASMY(W4ASM_BODY_Y_0);
       if constexpr (V == 1) W4_ASMY(W4ASM_BODY_Y_1);
       if constexpr (V == 2) W4_ASMY(W4ASM_BODY_Y_2);
-      if constexpr (V == 3) W4_ASMY(W4ASM_BODY_Y_3);
+
 
 
 
@@ -195,7 +195,6 @@ extern "C" int awq_w4asm(int var, const void *xs, const void *wq, const void *yr
   case 0: return go<0>(a, stream);
   case 1: return go<1>(a, stream);
   case 2: return go<2>(a, stream);
-  case 3: return go<3>(a, stream);
   default: return 3;
   }
 }
