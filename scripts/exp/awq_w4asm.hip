@@ -30,7 +30,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, uint
 
 template <int V>
 __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
-  constexpr int S = kW4Slots[V], EPI = kW4Epi[V], GM = kW4Gm[V];
+  constexpr int S = kW4Slots[V], EPI = kW4Epi[V], GM = kW4Gm[V] < 0 ? -kW4Gm[V] : kW4Gm[V];
+  constexpr bool XN = kW4Gm[V] < 0;
   __shared__ __attribute__((aligned(16))) unsigned char lds[S == 2 ? 131072 : S * 32768];  // S 2: the T64 schedule, two 64 KiB tile slots
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -42,7 +43,9 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
     constexpr int GN = 32 / GM;
     const int slot = li % 32, u = (li / 32) * 8 + xcd;
     const int mgn = (p.tiles_m + GM - 1) / GM, nn4 = (p.tiles_n + GN - 1) / GN;
-    const int mg = u % mgn, n4 = (u / mgn) % nn4;
+    // GM < 0 encodes the N-synchronised order: the 8 XCDs of a round share the X panels (same
+    // row group) and take consecutive column groups (different W panels)
+    const int mg = XN ? (u / nn4) % mgn : u % mgn, n4 = XN ? u % nn4 : (u / mgn) % nn4;
     g = u / (mgn * nn4);
     tm = mg * GM + slot % GM;
     tn = n4 * GN + slot / GM;
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(256) void w4asm_kernel(Args p) {
 
 // xs [G, M, K] pre-scaled activations, wq [G, N, K], yref [M, N] (bf16); partial [G * tiles]
 template <int V> int go(const Args &a, hipStream_t stream) {
-  constexpr int GM = kW4Gm[V], GN = 32 / GM;
+  constexpr int GM = kW4Gm[V] < 0 ? -kW4Gm[V] : kW4Gm[V], GN = 32 / GM;
   const int units = a.G * ((a.tiles_m + GM - 1) / GM) * ((a.tiles_n + GN - 1) / GN);
   w4asm_kernel<V><<<(unsigned)((units + 7) / 8 * 8 * 32), 256, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -34,8 +34,8 @@ SLOT = 32768
 # EPI 3: T64B (three fragment sets, two barriers per tile, DMAs two tiles ahead from the tile start)
 VARIANTS = [
     (2, "front/splitwx/0/a", 2, 0, 1, "", 3, 8),
-    (2, "win40/splitwx/0/f", 2, 0, 1, "", 3, 8),
-    (2, "win48/splitwx/0/g", 2, 0, 1, "", 3, 8),
+    (2, "front/splitwx/0/a", 2, 0, 1, "", 3, -8),
+    (2, "front/splitwx/0/a", 2, 0, 1, "", 3, -4),
 ]
 CACHE = ""
 
