@@ -384,10 +384,8 @@ int mtq_awq_search_gemm(const void *x, const void *sinv, const void *wq, const v
  * per-tile square-sum order): MTQ_AWQ_SEARCH_AUTO = what mtq_awq_search_gemm runs (W4 where its
  * limits allow, else PP); PP = the r03 two-group ping-pong kernel (8 waves, 128 x 64 per wave);
  * W4 = the r06 one-wave-per-SIMD kernel (4 waves, 128 x 128 per wave, K loop in generated inline
- * asm; needs K % 128 == 0 and M * N * 2 < 2^32, MTQ_ERR_INVALID_ARG otherwise); W4S = the W4
- * kernel with x * (1/s_g) applied to the X fragments inside the K loop (no pre-scale pass; bf16,
- * the W4 limits and (M + 256) * K * 2, (N + 256) * K * 2 < 2^32). */
-enum { MTQ_AWQ_SEARCH_AUTO = 0, MTQ_AWQ_SEARCH_PP = 1, MTQ_AWQ_SEARCH_W4 = 2, MTQ_AWQ_SEARCH_W4S = 3 };
+ * asm; needs K % 128 == 0 and M * N * 2 < 2^32, MTQ_ERR_INVALID_ARG otherwise). */
+enum { MTQ_AWQ_SEARCH_AUTO = 0, MTQ_AWQ_SEARCH_PP = 1, MTQ_AWQ_SEARCH_W4 = 2 };
 int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const void *wq, const void *bias,
                                const void *yref, int64_t M, int64_t N, int64_t K, int dtype, int G,
                                float *loss, float *workspace, int64_t workspace_floats, int kernel,

@@ -57,9 +57,6 @@ for name, (N, K) in SHAPES.items():
     def search():
         ops.awq_search_gemm(x, si, wq, None, yref, loss)
 
-    def search_s():
-        ops.awq_search_gemm(x, si, wq, None, yref, loss, 3)
-
     def search_pp():
         ops.awq_search_gemm(x, si, wq, None, yref, loss, 1)
 
@@ -79,7 +76,7 @@ for name, (N, K) in SHAPES.items():
         for g in range(G):
             F.linear(x, wq[g])
 
-    arms = {"fused": search, "fused_inloop_scale": search_s, "fused_pp": search_pp, "batched": batched, "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
+    arms = {"fused": search, "fused_pp": search_pp, "batched": batched, "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
     t = {k: [] for k in arms}
     for _ in range(ROUNDS):
         for k, f in arms.items():

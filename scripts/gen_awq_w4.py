@@ -142,189 +142,6 @@ def body(op):
     return L
 
 
-# ---- S form: x * (1/s_g) inside the K loop (no pre-scale pass; X read from x itself) ----------
-# The X fragments are scaled in place just before use, T(x * sinv) = v_cvt_pk_bf16_f32 of the
-# exact fp32 products (bf16 x bf16 fits fp32), the pre-scale pass's arithmetic bit for bit:
-# fragment i+1 of a phase while the MFMAs of row block i run (16 VALU each), fragment 0 of the
-# next phase at the end of the current one.  sinv of a K tile: two buffer_load_dwordx4 per lane
-# (its 8 k values of each k-half) with the tile's W DMAs, into a raw buffer by tile parity,
-# unpacked to fp32 pairs at the end of the previous tile.  bf16 only.
-U0, U1 = 28, 36            # sinv fp32 pairs of k-half 0 / 1 (8 VGPRs each)
-RAW = (44, 52)             # raw sinv of tiles of parity 0 / 1 (k0: +0..3, k1: +4..7)
-TMP = ((24, 25), (26, 27))  # fp32 pair temps of the scaling
-YT = (20, 21, 22, 23)      # yref DMA lane offsets, rotated
-XS_P1_DMAS = [8 * k + 1 for k in range(8)]
-XS_P1_SLOADS = [4, 12]
-XS_P2_DMAS = [33 + 4 * k for k in range(8)]
-XS_P2_READS = list(range(32))
-XS_SET = (64, 128, 192)
-
-
-def xf3(s, i):
-    return XS_SET[s] + 4 * i
-
-
-def wf3(s, j):
-    return XS_SET[s] + 32 + 4 * j
-
-
-def mfma3(op, s, i, j):
-    a = (i * 8 + j) * 4
-    return (f"{op} a[{a}:{a + 3}], v[{wf3(s, j)}:{wf3(s, j) + 3}], "
-            f"v[{xf3(s, i)}:{xf3(s, i) + 3}], a[{a}:{a + 3}]")
-
-
-def reads3(s, xb, wb):
-    out = []
-    for i in range(8):
-        out.append(f"ds_read_b128 v[{xf3(s, i)}:{xf3(s, i) + 3}], {xb} offset:{i * 2048}")
-        out.append(f"ds_read_b128 v[{wf3(s, i)}:{wf3(s, i) + 3}], {wb} offset:{i * 2048}")
-    return out
-
-
-def scale_frag(s, i, u):
-    """X fragment i of set s (4 dwords = 8 bf16, k = 8 fq + 0..7 of its k-half) times the k-half's
-    sinv pairs at v[u + 2 d : u + 2 d + 1]: 16 VALU."""
-    out = []
-    for d in range(4):
-        x = xf3(s, i) + d
-        t0, t1 = TMP[d & 1]
-        out += [f"v_lshlrev_b32 v{t0}, 16, v{x}", f"v_and_b32 v{t1}, 0xffff0000, v{x}",
-                f"v_pk_mul_f32 v[{t0}:{t1}], v[{t0}:{t1}], v[{u + 2 * d}:{u + 2 * d + 1}]",
-                f"v_cvt_pk_bf16_f32 v{x}, v{t0}, v{t1}"]
-    return out
-
-
-def spread(instrs, gaps=6):
-    """instrs over the gaps after the first `gaps` MFMAs of a row (3 3 3 3 2 2 for 16), then
-    s_nop 1: the last VALU write of a fragment is >= 2 MFMA issues before the MFMA that reads it
-    (VALU write -> MFMA SrcA/B needs two wait states)."""
-    out, k = [], 0
-    for g in range(gaps):
-        m = (len(instrs) - k + gaps - g - 1) // (gaps - g)
-        out.append(instrs[k:k + m])
-        k += m
-    out[-1] = out[-1] + ["s_nop 1"]
-    return out + [[]] * (8 - gaps)
-
-
-def unpack(raw, u):
-    """4 raw sinv dwords (8 bf16) -> 8 fp32 at v[u : u + 8]: 8 VALU."""
-    out = []
-    for d in range(4):
-        out += [f"v_lshlrev_b32 v{u + 2 * d}, 16, v{raw + d}", f"v_and_b32 v{u + 2 * d + 1}, 0xffff0000, v{raw + d}"]
-    return out
-
-
-def kdmas_s():
-    """16 DMAs of one K tile, X (from x) then W; the lane base %[xa|wa]{u & 1} and the scalar
-    offset kc + u * 16 K - (u % 4) KiB (the instruction offset carries the LDS block step)."""
-    out = []
-    for part, (rs, vo) in enumerate((("%[xr]", "xa"), ("%[wr]", "wa"))):
-        for u in range(8):
-            pre = [f"s_add_u32 m0, %[m0s], {part * 32768 + (u // 4) * 4096}", "s_nop 0"] if u % 4 == 0 else []
-            so = [f"s_mul_i32 %[kcu], %[k16], {u}", "s_add_u32 %[kcu], %[kcu], %[kc]"]
-            if u % 4:
-                so.append(f"s_sub_u32 %[kcu], %[kcu], {(u % 4) * 1024}")
-            out.append(pre + so + [f"buffer_load_dwordx4 %[{vo}{u & 1}], {rs}, %[kcu] offen offset:{(u % 4) * 1024} lds"])
-    return out
-
-
-def ydmas_s():
-    """yref DMAs with the lane's swizzled chunk computed here: ya + 16 ((l & 31) ^ ((2 k + (l >> 5)) & 15))."""
-    out = []
-    for u in range(16):
-        t = YT[u % 4]
-        out.append([f"s_add_u32 m0, %[m0y], {u * 1024}", f"s_mul_i32 %[yso], %[ys2], {u}",
-                    "s_add_u32 %[yso], %[yso], %[ybs]",
-                    f"v_add_u32 v{t}, {2 * (u % 8)}, %[yc]", f"v_and_b32 v{t}, 15, v{t}",
-                    f"v_xor_b32 v{t}, %[yb], v{t}", f"v_lshl_add_u32 v{t}, v{t}, 4, %[ya]",
-                    f"buffer_load_dwordx4 v{t}, %[yr], %[yso] offen lds"])
-    return out
-
-
-def sloads(parity):
-    r = RAW[parity]
-    return [[f"buffer_load_dwordx4 v[{r}:{r + 3}], %[sv], %[sr], %[kc] offen"],
-            [f"buffer_load_dwordx4 v[{r + 4}:{r + 7}], %[sv], %[sr], %[kc] offen offset:64"]]
-
-
-def tile_s(op, k1set, parity, yhalf=None):
-    """One K tile of the S form (tile parity = parity; its k-half 1 in set k1set)."""
-    nk1 = 3 - k1set
-    if yhalf is None:
-        L = ["s_add_u32 %[m0s], %[m0b], %[sdma]", "s_min_u32 %[kc], %[koff], %[klast]",
-             "s_add_u32 %[koff], %[koff], 128"]
-        dm = kdmas_s()
-    else:
-        L = ["s_add_u32 %[m0y], %[m0yb], %[sdma]",
-             "s_mov_b32 %[ybs], %[yrb]" if yhalf == 0 else "s_add_u32 %[ybs], %[yrb], %[yh]"]
-        dm = ydmas_s()
-    dm = dm[8:] + dm[:8]
-    sl = sloads(parity)  # the tile-after-next's sinv: same parity
-    # phase 1: MFMAs on A; scale A fragment i+1 during row i, the k-half-1 fragment 0 during row 7
-    va = []
-    for i in range(8):
-        va.append(spread(scale_frag(0, i + 1, U0) if i < 7 else scale_frag(k1set, 0, U1)))
-    for n in range(64):
-        L.append(mfma3(op, 0, n // 8, n % 8))
-        L += va[n // 8][n % 8]
-        if n in XS_P1_DMAS:
-            L += dm[XS_P1_DMAS.index(n)]
-        if n in XS_P1_SLOADS:
-            L += sl[XS_P1_SLOADS.index(n)]
-    L += ["s_waitcnt vmcnt(10)", "s_barrier", "s_xor_b32 %[srd], %[sdma], 65536",
-          "v_add_u32 v60, %[srd], %[xb0]", "v_add_u32 v61, %[srd], %[wb0]",
-          "v_add_u32 v62, %[srd], %[xb1]", "v_add_u32 v63, %[srd], %[wb1]"]
-    rd = reads3(0, "v60", "v61") + reads3(nk1, "v62", "v63")
-    # phase 2: MFMAs on k1set; scale its fragment i+1 during row i (rows 0-6); the next tile's sinv
-    # k-half 0 unpacked in rows 4-5 (U0 is free in phase 2), k-half 1 in row 7 (after U1's last
-    # use), then the next tile's A fragment 0 (its read is one of the first 17 of 32)
-    nraw = RAW[1 - parity]
-    vb = [spread(scale_frag(k1set, i + 1, U1)) for i in range(7)]
-    for n in range(64):
-        L.append(mfma3(op, k1set, n // 8, n % 8))
-        if n // 8 < 7:
-            L += vb[n // 8][n % 8]
-        if n == 36:
-            L += unpack(nraw, U0)
-        if n == 56:
-            L += unpack(nraw + 4, U1) + ["s_waitcnt lgkmcnt(15)"]
-        if n >= 57:
-            L += scale_frag(0, 0, U0)[(n - 57) * 3:(n - 57) * 3 + 3] if n < 63 else scale_frag(0, 0, U0)[18:]
-        if n in XS_P2_READS:
-            L.append(rd[XS_P2_READS.index(n)])
-        if n in XS_P2_DMAS:
-            L += dm[8 + XS_P2_DMAS.index(n)]
-    L += ["s_waitcnt lgkmcnt(0)", "s_barrier", "s_xor_b32 %[sdma], %[sdma], 65536"]
-    return L
-
-
-def body_s(op):
-    L = ["s_nop 4", "s_mov_b32 %[koff], 0", "s_mov_b32 %[sdma], 0"]
-    for t in range(2):
-        L += ["s_min_u32 %[kc], %[koff], %[klast]", "s_add_u32 %[koff], %[koff], 128",
-              f"s_add_u32 %[m0s], %[m0b], {t * 65536}"]
-        for d in kdmas_s():
-            L += d
-        for d in sloads(t):
-            L += d
-    L += [f"v_accvgpr_write_b32 a{r}, 0" for r in range(256)]
-    L += ["s_nop 2", "s_waitcnt vmcnt(18)", "s_barrier"]  # tile 0 and its sinv landed
-    L += unpack(RAW[0], U0) + unpack(RAW[0] + 4, U1)
-    L += reads3(0, "%[xb0]", "%[wb0]") + reads3(1, "%[xb1]", "%[wb1]")
-    L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
-    L += scale_frag(0, 0, U0)
-    L += ["s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_tail_%="]
-    L.append("L_w4_loop_%=:")
-    L += tile_s(op, 1, 0) + tile_s(op, 2, 1)
-    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 L_w4_loop_%="]
-    L.append("L_w4_tail_%=:")
-    L += tile_s(op, 1, 0, 0) + tile_s(op, 2, 1, 1)
-    L += ["s_waitcnt vmcnt(0)", "s_waitcnt lgkmcnt(0)", "s_barrier", "s_nop 15", "s_nop 15", "s_nop 15"]
-    return L
-
-
 def text():
     t = "// generated by scripts/gen_awq_w4.py -- do not edit\n"
     for key, op in MFMA.items():
@@ -332,11 +149,6 @@ def text():
         t += f"#define MTQ_W4_BODY_{key} \\\n" + asm.replace("\n", " \\\n") + "\n"
     clob = ", ".join(f'"v{r}"' for r in range(60, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
     t += "#define MTQ_W4_CLOBBERS " + clob.replace("\n", " \\\n") + ', "memory", "scc"\n'
-    # the S form (x * (1/s) in the loop): bf16 only, its own register map (v[20:255] named)
-    asm = "".join(f'  "{ln}\\n\\t"\n' for ln in body_s(MFMA["BF16"]))
-    t += "#define MTQ_W4S_BODY_BF16 \\\n" + asm.replace("\n", " \\\n") + "\n"
-    clob = ", ".join(f'"v{r}"' for r in range(20, 256)) + ",\n  " + ", ".join(f'"a{r}"' for r in range(256))
-    t += "#define MTQ_W4S_CLOBBERS " + clob.replace("\n", " \\\n") + ', "memory", "scc"\n'
     for i in range(8):  # the 32 accumulators of row block i into float o[32]
         rd = " ".join(f'asm volatile("v_accvgpr_read_b32 %0, a{32 * i + r}" : "=v"(o[{r}]));' for r in range(32))
         t += f"#define MTQ_W4_STRIP_{i}(o) {rd}\n"

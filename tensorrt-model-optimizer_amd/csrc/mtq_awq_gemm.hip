@@ -385,9 +385,7 @@ __global__ __launch_bounds__(kThreads) void awq_search_pp_kernel(AwqGemmArgs p) 
 typedef float w4f2 __attribute__((ext_vector_type(2)));
 typedef __bf16 w4b2 __attribute__((ext_vector_type(2)));
 
-// SCALE (bf16 only): the S form -- p.x is x itself and x * (1/s_g) is applied to the X fragments
-// inside the K loop (gen_awq_w4.py body_s), so no pre-scale pass and no [G, M, K] buffer.
-template <typename T, bool HAS_BIAS, bool SCALE = false>
+template <typename T, bool HAS_BIAS>
 __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[131072];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -408,106 +406,65 @@ __global__ __launch_bounds__(256) void awq_search_w4_kernel(AwqGemmArgs p) {
   const int tile = tm * p.tiles_n + tn;
   const int64_t m0 = (int64_t)tm * kBM, n0 = (int64_t)tn * kBN;
   const int64_t K = p.K;
-  if constexpr (SCALE) {
-    // X from x (every alpha), rows past M / N read as zero through the descriptors' sizes (no
-    // clamp: the lane bases are then linear in the DMA index u, carried by the scalar offset)
-    const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
-    const __amdgpu_buffer_rsrc_t xr = wave_rsrc(p.x, (uint32_t)(p.M * K * 2));
-    const __amdgpu_buffer_rsrc_t wr = wave_rsrc(W, (uint32_t)(p.N * K * 2));
-    const __amdgpu_buffer_rsrc_t sr = wave_rsrc(reinterpret_cast<const T *>(p.sinv) + (int64_t)g * K, (uint32_t)(K * 2));
-    const __amdgpu_buffer_rsrc_t yr = wave_rsrc(p.yref, (uint32_t)(p.M * p.N * 2));
-    const unsigned r0 = 64 * wave + (lane >> 3), c0 = (lane & 7) ^ ((r0 >> 1) & 7);
-    const unsigned Ku = (unsigned)K;
-    const unsigned xa0 = (((unsigned)m0 + r0) * Ku + 8 * c0) * 2, xa1 = (((unsigned)m0 + r0) * Ku + 8 * (c0 ^ 4)) * 2;
-    const unsigned wa0 = (((unsigned)n0 + r0) * Ku + 8 * c0) * 2, wa1 = (((unsigned)n0 + r0) * Ku + 8 * (c0 ^ 4)) * 2;
-    const unsigned k16 = __builtin_amdgcn_readfirstlane(16u * Ku);
-    const unsigned sv = 16u * (unsigned)(lane >> 4);
-    const unsigned lds0 = (unsigned)(uintptr_t)lds;
-    const int fr_ = lane & 15, fq_ = lane >> 4;
-    const unsigned lt0 = fr_ * 128 + ((fq_ ^ ((fr_ >> 1) & 7)) << 4);
-    const unsigned lt1 = fr_ * 128 + (((4 + fq_) ^ ((fr_ >> 1) & 7)) << 4);
-    const unsigned xb0 = lds0 + wm * 16384 + lt0, xb1 = lds0 + wm * 16384 + lt1;
-    const unsigned wb0 = lds0 + 32768 + wn * 16384 + lt0, wb1 = lds0 + 32768 + wn * 16384 + lt1;
-    const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + wave * 8192);
-    const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
-    unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 2) / 2));
-    const unsigned yrb = __builtin_amdgcn_readfirstlane((unsigned)(((m0 + 32 * wave) * p.N + n0) * 2));
-    const unsigned yh = __builtin_amdgcn_readfirstlane((unsigned)(128 * p.N * 2));
-    const unsigned ys2 = __builtin_amdgcn_readfirstlane((unsigned)(2 * p.N * 2));
-    const unsigned m0yb = __builtin_amdgcn_readfirstlane(lds0 + wave * 16384);
-    const unsigned ya = (unsigned)((lane >> 5) * p.N * 2), yb = lane & 31, yc = lane >> 5;
-    unsigned koff, kc, kcu, m0s, sdma, srd, m0y, yso, ybs;
-    asm volatile(MTQ_W4S_BODY_BF16
-                 : [koff] "=&s"(koff), [kc] "=&s"(kc), [kcu] "=&s"(kcu), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma),
-                   [srd] "=&s"(srd), [cnt] "+s"(cnt), [m0y] "=&s"(m0y), [yso] "=&s"(yso), [ybs] "=&s"(ybs)
-                 : [xr] "s"(xr), [wr] "s"(wr), [sr] "s"(sr), [m0b] "s"(m0b), [klast] "s"(klast), [k16] "s"(k16),
-                   [xa0] "v"(xa0), [xa1] "v"(xa1), [wa0] "v"(wa0), [wa1] "v"(wa1), [sv] "v"(sv),
-                   [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1),
-                   [yr] "s"(yr), [yrb] "s"(yrb), [yh] "s"(yh), [ys2] "s"(ys2), [m0yb] "s"(m0yb),
-                   [ya] "v"(ya), [yb] "v"(yb), [yc] "v"(yc)
-                 : MTQ_W4S_CLOBBERS);
-  } else {
-    const T *X = reinterpret_cast<const T *>(p.x) + (int64_t)g * p.M * K;
-    const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
-    const __amdgpu_buffer_rsrc_t xr = wave_rsrc(X, (uint32_t)(p.M * K * 2));
-    const __amdgpu_buffer_rsrc_t wr = wave_rsrc(W, (uint32_t)(p.N * K * 2));
-    const __amdgpu_buffer_rsrc_t yr = wave_rsrc(p.yref, (uint32_t)(p.M * p.N * 2));
+  const T *X = reinterpret_cast<const T *>(p.x) + (int64_t)g * p.M * K;
+  const T *W = reinterpret_cast<const T *>(p.wq) + (int64_t)g * p.N * K;
+  const __amdgpu_buffer_rsrc_t xr = wave_rsrc(X, (uint32_t)(p.M * K * 2));
+  const __amdgpu_buffer_rsrc_t wr = wave_rsrc(W, (uint32_t)(p.N * K * 2));
+  const __amdgpu_buffer_rsrc_t yr = wave_rsrc(p.yref, (uint32_t)(p.M * p.N * 2));
 
-    // K-tile DMA sources: wave w fills 1 KiB blocks w*8 + u of each operand's 32 KiB tile part (8
-    // rows of 128 B); lane l writes row 64 w + 8 u + (l >> 3), stored chunk l & 7 = source chunk
-    // c ^ ((row >> 1) & 7).  The instruction offset carries the block step (u % 4) KiB: subtracted here.
-    unsigned xo[8], wo[8];
+  // K-tile DMA sources: wave w fills 1 KiB blocks w*8 + u of each operand's 32 KiB tile part (8
+  // rows of 128 B); lane l writes row 64 w + 8 u + (l >> 3), stored chunk l & 7 = source chunk
+  // c ^ ((row >> 1) & 7).  The instruction offset carries the block step (u % 4) KiB: subtracted here.
+  unsigned xo[8], wo[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = 64 * wave + 8 * u + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const int64_t row = m0 + r < p.M ? m0 + r : p.M - 1;
-      const int64_t col = n0 + r < p.N ? n0 + r : p.N - 1;
-      xo[u] = (unsigned)((row * K + 8 * c) * 2) - (unsigned)((u % 4) * 1024);
-      wo[u] = (unsigned)((col * K + 8 * c) * 2) - (unsigned)((u % 4) * 1024);
-    }
-    // fragment reads: row 16 i + fr of the wave's block, 16-byte chunk 4 s + fq of k-half s
-    const int fr = lane & 15, fq = lane >> 4;
-    const unsigned lds0 = (unsigned)(uintptr_t)lds;
-    const unsigned lt0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) << 4);
-    const unsigned lt1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) << 4);
-    const unsigned xb0 = lds0 + wm * 16384 + lt0, xb1 = lds0 + wm * 16384 + lt1;
-    const unsigned wb0 = lds0 + 32768 + wn * 16384 + lt0, wb1 = lds0 + 32768 + wn * 16384 + lt1;
-    const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + wave * 8192);
-    const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
-    unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 2) / 2));  // two tiles per pass
-    // reference-tile DMA sources: half h (rows 128 h ..) lands in slot (K / 64 + h) % 2; wave w
-    // fills rows 32 w + 2 u + (l >> 5), u = 0..15, row r's 16-byte chunk c at c ^ (r & 15)
-    const unsigned yrb = __builtin_amdgcn_readfirstlane((unsigned)(((m0 + 32 * wave) * p.N + n0) * 2));
-    const unsigned yh = __builtin_amdgcn_readfirstlane((unsigned)(128 * p.N * 2));
-    const unsigned ys2 = __builtin_amdgcn_readfirstlane((unsigned)(2 * p.N * 2));
-    const unsigned m0yb = __builtin_amdgcn_readfirstlane(lds0 + wave * 16384);
-    unsigned yo[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
-    unsigned koff, kc, m0s, sdma, srd, m0y, yso, ybs;
-#define MTQ_W4_ASM(BODY)                                                                              \
-    asm volatile(BODY                                                                                   \
-                 : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
-                   [cnt] "+s"(cnt), [m0y] "=&s"(m0y), [yso] "=&s"(yso), [ybs] "=&s"(ybs)                 \
-                 : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast),                         \
-                   [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]),                  \
-                   [xo4] "v"(xo[4]), [xo5] "v"(xo[5]), [xo6] "v"(xo[6]), [xo7] "v"(xo[7]),                  \
-                   [wo0] "v"(wo[0]), [wo1] "v"(wo[1]), [wo2] "v"(wo[2]), [wo3] "v"(wo[3]),                  \
-                   [wo4] "v"(wo[4]), [wo5] "v"(wo[5]), [wo6] "v"(wo[6]), [wo7] "v"(wo[7]),                  \
-                   [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1),                           \
-                   [yr] "s"(yr), [yrb] "s"(yrb), [yh] "s"(yh), [ys2] "s"(ys2), [m0yb] "s"(m0yb),             \
-                   [yo0] "v"(yo[0]), [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]),                  \
-                   [yo4] "v"(yo[4]), [yo5] "v"(yo[5]), [yo6] "v"(yo[6]), [yo7] "v"(yo[7])                   \
-                 : MTQ_W4_CLOBBERS)
-    if constexpr (sizeof(T) == 2 && __is_same(T, __bf16))
-      MTQ_W4_ASM(MTQ_W4_BODY_BF16);
-    else
-      MTQ_W4_ASM(MTQ_W4_BODY_F16);
-#undef MTQ_W4_ASM
+  for (int u = 0; u < 8; ++u) {
+    const int r = 64 * wave + 8 * u + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t row = m0 + r < p.M ? m0 + r : p.M - 1;
+    const int64_t col = n0 + r < p.N ? n0 + r : p.N - 1;
+    xo[u] = (unsigned)((row * K + 8 * c) * 2) - (unsigned)((u % 4) * 1024);
+    wo[u] = (unsigned)((col * K + 8 * c) * 2) - (unsigned)((u % 4) * 1024);
   }
+  // fragment reads: row 16 i + fr of the wave's block, 16-byte chunk 4 s + fq of k-half s
   const int fr = lane & 15, fq = lane >> 4;
+  const unsigned lds0 = (unsigned)(uintptr_t)lds;
+  const unsigned lt0 = fr * 128 + ((fq ^ ((fr >> 1) & 7)) << 4);
+  const unsigned lt1 = fr * 128 + (((4 + fq) ^ ((fr >> 1) & 7)) << 4);
+  const unsigned xb0 = lds0 + wm * 16384 + lt0, xb1 = lds0 + wm * 16384 + lt1;
+  const unsigned wb0 = lds0 + 32768 + wn * 16384 + lt0, wb1 = lds0 + 32768 + wn * 16384 + lt1;
+  const unsigned m0b = __builtin_amdgcn_readfirstlane(lds0 + wave * 8192);
+  const unsigned klast = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 1) * 128));
+  unsigned cnt = __builtin_amdgcn_readfirstlane((unsigned)((K / 64 - 2) / 2));  // two tiles per pass
+  // reference-tile DMA sources: half h (rows 128 h ..) lands in slot (K / 64 + h) % 2; wave w
+  // fills rows 32 w + 2 u + (l >> 5), u = 0..15, row r's 16-byte chunk c at c ^ (r & 15)
+  const unsigned yrb = __builtin_amdgcn_readfirstlane((unsigned)(((m0 + 32 * wave) * p.N + n0) * 2));
+  const unsigned yh = __builtin_amdgcn_readfirstlane((unsigned)(128 * p.N * 2));
+  const unsigned ys2 = __builtin_amdgcn_readfirstlane((unsigned)(2 * p.N * 2));
+  const unsigned m0yb = __builtin_amdgcn_readfirstlane(lds0 + wave * 16384);
+  unsigned yo[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    yo[k] = (unsigned)((lane >> 5) * p.N * 2) + 16u * (unsigned)((lane & 31) ^ ((2 * k + (lane >> 5)) & 15));
+  unsigned koff, kc, m0s, sdma, srd, m0y, yso, ybs;
+#define MTQ_W4_ASM(BODY)                                                                              \
+  asm volatile(BODY                                                                                   \
+               : [koff] "=&s"(koff), [kc] "=&s"(kc), [m0s] "=&s"(m0s), [sdma] "=&s"(sdma), [srd] "=&s"(srd), \
+                 [cnt] "+s"(cnt), [m0y] "=&s"(m0y), [yso] "=&s"(yso), [ybs] "=&s"(ybs)                 \
+               : [xr] "s"(xr), [wr] "s"(wr), [m0b] "s"(m0b), [klast] "s"(klast),                         \
+                 [xo0] "v"(xo[0]), [xo1] "v"(xo[1]), [xo2] "v"(xo[2]), [xo3] "v"(xo[3]),                  \
+                 [xo4] "v"(xo[4]), [xo5] "v"(xo[5]), [xo6] "v"(xo[6]), [xo7] "v"(xo[7]),                  \
+                 [wo0] "v"(wo[0]), [wo1] "v"(wo[1]), [wo2] "v"(wo[2]), [wo3] "v"(wo[3]),                  \
+                 [wo4] "v"(wo[4]), [wo5] "v"(wo[5]), [wo6] "v"(wo[6]), [wo7] "v"(wo[7]),                  \
+                 [xb0] "v"(xb0), [xb1] "v"(xb1), [wb0] "v"(wb0), [wb1] "v"(wb1),                           \
+                 [yr] "s"(yr), [yrb] "s"(yrb), [yh] "s"(yh), [ys2] "s"(ys2), [m0yb] "s"(m0yb),             \
+                 [yo0] "v"(yo[0]), [yo1] "v"(yo[1]), [yo2] "v"(yo[2]), [yo3] "v"(yo[3]),                  \
+                 [yo4] "v"(yo[4]), [yo5] "v"(yo[5]), [yo6] "v"(yo[6]), [yo7] "v"(yo[7])                   \
+               : MTQ_W4_CLOBBERS)
+  if constexpr (sizeof(T) == 2 && __is_same(T, __bf16))
+    MTQ_W4_ASM(MTQ_W4_BODY_BF16);
+  else
+    MTQ_W4_ASM(MTQ_W4_BODY_F16);
+#undef MTQ_W4_ASM
 
   // ---- epilogue.  A lane's accumulators of tile (i, j) are out[m][n .. n+3], m = 16 i + fr, n =
   // 16 j + 4 fq of the wave's block (a[32 i + 4 j ..]); bias, output and difference rounded to T,
@@ -719,7 +676,7 @@ extern "C" int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const
                                           const void *yref, int64_t M, int64_t N, int64_t K, int dtype,
                                           int G, float *loss, float *workspace, int64_t workspace_floats,
                                           int kernel, hipStream_t stream) {
-  if (kernel < MTQ_AWQ_SEARCH_AUTO || kernel > MTQ_AWQ_SEARCH_W4S) return MTQ_ERR_INVALID_ARG;
+  if (kernel < MTQ_AWQ_SEARCH_AUTO || kernel > MTQ_AWQ_SEARCH_W4) return MTQ_ERR_INVALID_ARG;
   if (M < 1 || N < 1 || K < kBK || K % kBK != 0 || G < 1 || G > 64) return MTQ_ERR_INVALID_ARG;
   if (!x || !sinv || !wq || !yref || !loss || !workspace) return MTQ_ERR_INVALID_ARG;
   if (dtype != MTQ_BF16 && dtype != MTQ_F16) return MTQ_ERR_DTYPE;
@@ -731,26 +688,6 @@ extern "C" int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const
   if (workspace_floats < mtq_awq_search_gemm_workspace_floats(M, N, K, G) ||
       tiles * G > (int64_t)INT32_MAX / 4)
     return MTQ_ERR_INVALID_ARG;
-  // 32 slots per 8 x 4 tile unit, units padded to a multiple of the 8 XCDs (see the kernel)
-  const int64_t units = (int64_t)G * ((tiles_m + 7) / 8) * ((tiles_n + 3) / 4);
-  const dim3 grid((unsigned)((units + 7) / 8 * 8 * 32));
-  const bool w4_ok = K >= 128 && K % 128 == 0 && M * N * 2 < ((int64_t)1 << 32);
-  if (kernel == MTQ_AWQ_SEARCH_W4S) {
-    // x * (1/s_g) inside the K loop: bf16, the W4 limits, and 32-bit row offsets up to a tile past M / N
-    if (!w4_ok || dtype != MTQ_BF16 || (M + kBM) * K * 2 >= ((int64_t)1 << 32) || (N + kBN) * K * 2 >= ((int64_t)1 << 32))
-      return MTQ_ERR_INVALID_ARG;
-    AwqGemmArgs a{x, sinv, wq, bias, yref, workspace, M, N, K, (int)tiles_m, (int)tiles_n, G};
-    count_dispatch(kDispAwqSearchW4);
-    if (bias)
-      awq_search_w4_kernel<__bf16, true, true><<<grid, 256, 0, stream>>>(a);
-    else
-      awq_search_w4_kernel<__bf16, false, true><<<grid, 256, 0, stream>>>(a);
-    int st = host_check_launch();
-    if (st != MTQ_OK) return st;
-    awq_search_finish_kernel<<<(unsigned)G, 256, 0, stream>>>(workspace, (int)tiles, G, 1.0 / ((double)M * (double)N),
-                                                    loss);
-    return host_check_launch();
-  }
   // x * (1/s_g) for every alpha into the workspace (the reference's bf16 multiply, one read of x)
   void *xs = workspace + partial_floats(M, N, G);
   if (dtype == MTQ_BF16)
@@ -760,6 +697,10 @@ extern "C" int mtq_awq_search_gemm_kernel(const void *x, const void *sinv, const
   int st0 = host_check_launch();
   if (st0 != MTQ_OK) return st0;
   AwqGemmArgs a{xs, sinv, wq, bias, yref, workspace, M, N, K, (int)tiles_m, (int)tiles_n, G};
+  // 32 slots per 8 x 4 tile unit, units padded to a multiple of the 8 XCDs (see the kernel)
+  const int64_t units = (int64_t)G * ((tiles_m + 7) / 8) * ((tiles_n + 3) / 4);
+  const dim3 grid((unsigned)((units + 7) / 8 * 8 * 32));
+  const bool w4_ok = K >= 128 && K % 128 == 0 && M * N * 2 < ((int64_t)1 << 32);
   if (kernel == MTQ_AWQ_SEARCH_W4 && !w4_ok) return MTQ_ERR_INVALID_ARG;
   if (kernel == MTQ_AWQ_SEARCH_W4 || (kernel == MTQ_AWQ_SEARCH_AUTO && w4_ok)) {
     count_dispatch(kDispAwqSearchW4);

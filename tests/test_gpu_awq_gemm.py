@@ -46,17 +46,15 @@ def _host_loss(x, sinv, wq, bias, yref):
     return torch.tensor(out, dtype=torch.float64).float()
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("kernel", [1, 2])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(256, 256, 64), (300, 320, 192), (512, 768, 256), (37, 1024, 128),
                                    (1000, 520, 640)])
 @pytest.mark.parametrize("with_bias", [False, True])
 def test_exact_integer_data(gpu, dtype, shape, with_bias, kernel):
     M, N, K = shape
-    if kernel >= 2 and K % 128:
+    if kernel == 2 and K % 128:
         pytest.skip("the W4 kernel needs K % 128 == 0 (test_kernel_choice covers the rejection)")
-    if kernel == 3 and dtype != torch.bfloat16:
-        pytest.skip("the in-loop scaling form is bf16 only")
     G = 3
     g = torch.Generator().manual_seed(M + N + K)
     # sparse small integers: every product sum, output, difference and square sum (per lane,
@@ -108,10 +106,6 @@ def test_llama_shapes_vs_unfused(gpu, nk, kernel):
     other = torch.zeros(G, device=gpu)
     ops().awq_search_gemm(x, sinv, wq, bias, yref, other, 3 - kernel)
     torch.testing.assert_close(loss, other, rtol=1e-5, atol=0)
-    if kernel == 2:  # x * (1/s) inside the K loop: the pre-scale pass's bf16 products, bit for bit
-        s3 = torch.zeros(G, device=gpu)
-        ops().awq_search_gemm(x, sinv, wq, bias, yref, s3, 3)
-        assert torch.equal(s3, loss)
 
 
 def test_kernel_choice(gpu):
@@ -136,11 +130,6 @@ def test_kernel_choice(gpu):
         ops().awq_search_gemm(torch.zeros(256, 64, device=gpu, dtype=dt), torch.ones(2, 64, device=gpu, dtype=dt),
                               torch.zeros(2, 256, 64, device=gpu, dtype=dt), None,
                               torch.zeros(256, 256, device=gpu, dtype=dt), torch.zeros(2, device=gpu), 2)
-    with pytest.raises(RuntimeError):  # the in-loop scaling form: bf16 only
-        h = torch.float16
-        ops().awq_search_gemm(torch.zeros(256, 128, device=gpu, dtype=h), torch.ones(2, 128, device=gpu, dtype=h),
-                              torch.zeros(2, 256, 128, device=gpu, dtype=h), None,
-                              torch.zeros(256, 256, device=gpu, dtype=h), torch.zeros(2, device=gpu), 3)
 
 
 def test_rejects_unsupported(gpu):
