@@ -436,6 +436,16 @@ _AWQ_FUSED = os.environ.get("MTQ_AMD_AWQ_FUSED", "auto")
 _AWQ_FUSED_CHOICES = ("auto", "always", "library", "never")
 
 
+def _awq_use_fused(m_rows: int, n_out: int, k_in: int, n_alpha: int, mode: str | None = None) -> bool:
+    """Route one linear's AWQ search: the fused MFMA kernel (mtq_awq_search_gemm) or the batched
+    hipBLASLt path.  The kernel's limits: G <= 64 alphas, 32-bit element offsets.  "auto": fused
+    where N <= 2048 or K <= N (measured faster there, DESIGN.md §4e r06 -- k/v, q/o, gate/up of
+    Llama-3-8B; down_proj, K > N, keeps the library)."""
+    mode = _AWQ_FUSED if mode is None else mode
+    ok = n_alpha <= _AWQ_FUSED_MAX_G and m_rows * k_in < 2**31 and n_out * k_in < 2**31
+    return ok and (mode == "always" or (mode == "auto" and (n_out <= _AWQ_FUSED_MAX_N or k_in <= n_out)))
+
+
 def _check_awq_fused() -> None:
     """Validate MTQ_AMD_AWQ_FUSED where it is used (awq_lite); a misspelt value only warns at
     import, so workflows that never reach the AWQ search are not broken by it."""
@@ -497,12 +507,7 @@ def _awq_search_fast(self, helper, input, out_act, blk) -> bool:
     bias = self.bias.detach() if self.bias is not None else None
     x2 = input.reshape(-1, input.shape[-1])
     n_out, k_in, n_alpha = w.shape[0], w.shape[1], len(helper.alphas)
-    # the fused kernel's limits (mtq_awq_search_gemm: G <= 64, 32-bit element offsets); the
-    # batched path's loss pass takes G <= 16; anything else runs one alpha at a time
-    fused_ok = n_alpha <= _AWQ_FUSED_MAX_G and x2.shape[0] * k_in < 2**31 and n_out * k_in < 2**31
-    fused = fused_ok and (_AWQ_FUSED == "always" or
-                          (_AWQ_FUSED == "auto" and (n_out <= _AWQ_FUSED_MAX_N or k_in <= n_out)))
-    if fused:
+    if _awq_use_fused(x2.shape[0], n_out, k_in, n_alpha):
         ops.awq_search_gemm(x2, sinv, wq, bias, out_act.reshape(-1, w.shape[0]), helper.loss)
     elif n_alpha <= 16:
         # wide linears: x * (1/s) for every alpha in one pass, one hipBLASLt GEMM per alpha into
