@@ -105,6 +105,15 @@ __device__ __forceinline__ float e2m1_mag(float a) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// v < 448 ? v : 448 for v >= +0 or a quiet NaN in ONE v_min_f32 (IEEE minNum returns the non-NaN
+// operand: NaN -> 448, as the compare form; -0 stays -0); the compiler's form was v_cmp +
+// v_cndmask
+__device__ __forceinline__ float min448(float v) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(kE4M3Max));
+  return r;
+}
+
 // RN(a / s) for a pair of a >= +0 (or NaN) on the packed fp32 ALU: div_rn (mtq_device.hpp) without
 // its copysign -- p never is -0 -- two quotients per v_pk_mul / v_pk_fma
 __device__ __forceinline__ f2v div_rn_pos2(f2v q, float s, float r) {
@@ -417,8 +426,8 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
 #pragma unroll
         for (int j = 0; j < 16; j += 2) {
           f2v v = div_rn_pos2(f2v{p[j], p[j + 1]}, a.p_scale, rs_p);
-          v.x = v.x < kE4M3Max ? v.x : kE4M3Max;  // NaN -> 448, as the scalar form
-          v.y = v.y < kE4M3Max ? v.y : kE4M3Max;
+          v.x = min448(v.x);  // NaN -> 448, as the scalar form
+          v.y = min448(v.y);
           const int c8 = __builtin_amdgcn_cvt_pk_fp8_f32(v.x, v.y, 0, false);
           const f2v r = __builtin_amdgcn_cvt_pk_f32_fp8(c8, false) * sp2;
           p[j] = r.x;
@@ -573,6 +582,53 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
   }
 
   // ---- o = acc / max(l, 1e-6); lane holds d = 32 d + crow(e, hi) of query row qrow
+  if constexpr (!F32 && DP == D && !FACT) {
+    // 16-bit output, d blocks of 32, staged through the K image (free: every wave passed the
+    // last stage's barrier) so it leaves as whole rows.  Lane hi = 0 holds columns 8k .. 8k+3 of
+    // its row and its partner (hi = 1) 8k+4 .. 8k+7, k = 4 d + e4; one v_permlane32_swap per
+    // dword of the groups (k, k+1) gives the low half columns 8k .. 8k+7 and the high half
+    // 8k+8 .. 8k+15 (guide T21), written as ds_write_b128 into this wave's 32 rows at the K pitch
+    // (conflict-free); read back 16 B per lane, CR chunks of a row on consecutive lanes, and
+    // stored with 64 / CR whole rows per instruction.  Per-lane row stores at the row stride
+    // (16 dwordx2, 32-64 rows each) made the epilogue ~4.5 k cycles per pass (r06 stamps,
+    // scripts/exp/bench_attn_exp.py): store-issue bound.
+    if (!active) return;  // wave-uniform
+    unsigned char *const ob = Ks + wave * 32 * PITCH;
+    if (qrow < lq) {
+      const float den = l > 1e-6f ? l : 1e-6f;
+      const float rden = 1.0f / den;
+      const f2v sv = {den, den}, rv = {rden, rden};
+#pragma unroll
+      for (int k = 0; k < 4 * DB; k += 2) {  // 8-column groups k, k + 1 (one pair live at a time)
+        uint32_t w[2][2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int i = 0; i < 4; i += 2) {  // div_rn on packed pairs (same ops, same copysign)
+            const int d = (k + g) >> 2, e = 4 * ((k + g) & 3) + i;
+            const f2v qv = {acc[d][e], acc[d][e + 1]};
+            const f2v y0 = qv * rv;
+            const f2v y = __builtin_elementwise_fma(__builtin_elementwise_fma(-y0, sv, qv), rv, y0);
+            // both halves in one v_cvt_pk (RNE, as Elem<T>::st twice; no shift / or)
+            w[g][i / 2] = pack2<T>(__builtin_copysignf(y.x, qv.x), __builtin_copysignf(y.y, qv.y));
+          }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const auto r = __builtin_amdgcn_permlane32_swap(w[0][j], w[1][j], false, false);
+          w[0][j] = r[0];
+          w[1][j] = r[1];
+        }
+        *reinterpret_cast<uint4 *>(ob + fr * PITCH + 16 * k + 16 * hi) = make_uint4(w[0][0], w[0][1], w[1][0], w[1][1]);
+      }
+    }
+#pragma unroll
+    for (int c = lane; c < 32 * CR; c += 64) {  // 32 * CR is a multiple of 64 (D % 16 == 0)
+      const int row = c / CR, ch = c - row * CR;
+      const uint4 v = *reinterpret_cast<const uint4 *>(ob + row * PITCH + ch * 16);
+      if (q0 + row < lq) *reinterpret_cast<uint4 *>(O + (int64_t)(q0 + row) * a.ot + ch * EC) = v;
+    }
+    return;
+  }
   if (active && qrow < lq) {
     const float den = l > 1e-6f ? l : 1e-6f;
     const float rden = 1.0f / den;

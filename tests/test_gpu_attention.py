@@ -76,7 +76,9 @@ def test_kernel_matches_reference_triton_kernel(gpu, gold, name):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("p_qdq,amax", [(None, 1.0), ("fp8", 1.0), ("fp8", 0.37), ("nvfp4", 1.0), ("nvfp4", 0.8)])
+# fp8 amax 0.01 / 1e-30: p / S past 448 on most keys (the saturating clamp, v_min_f32)
+@pytest.mark.parametrize("p_qdq,amax", [(None, 1.0), ("fp8", 1.0), ("fp8", 0.37), ("fp8", 0.01), ("fp8", 1e-30),
+                                        ("nvfp4", 1.0), ("nvfp4", 0.8)])
 def test_kernel_matches_oracle(gpu, dtype, d, p_qdq, amax):
     """Multi-block shapes: 2 sequences (300 and 161 tokens), GQA 8:2, several 128-row tiles."""
     from modelopt_amd.torch.kernels.common.attention import attention
