@@ -4,7 +4,11 @@
 from pathlib import Path
 
 R = Path(__file__).resolve().parents[2]
-s = (R / "tensorrt-model-optimizer_amd/csrc/mtq_attention.hip").read_text()
+import subprocess, sys
+src = "tensorrt-model-optimizer_amd/csrc/mtq_attention.hip"
+# optional git revision: the copy built from that commit (A/B against the working tree product)
+s = (subprocess.run(["git", "-C", str(R), "show", f"{sys.argv[1]}:{src}"], check=True, capture_output=True, text=True).stdout
+     if len(sys.argv) > 1 else (R / src).read_text())
 
 
 def sub(old, new):
