@@ -540,39 +540,7 @@ __device__ __forceinline__ void attn_tile(const AttnArgs &a, int b, int h, int k
     const int kvs = t * kStage;
     f32x16 s_a, s_b;  // scores of the stage's two 32-key tiles (fixed registers, no copies)
     if (AHEAD && active && kvs < w_end) s_a = score(0);
-    // both 32-key tiles of the stage live for this wave (the usual case): their softmax chains
-    // interleaved -- the max of tile b needs only tile a's max, its exps / sum / P qdq nothing of
-    // tile a -- with every operation and its order per tile unchanged (the reference's per-tile
-    // update: m, l, acc * corr then P . V, tile a before tile b), so the ALU sees two independent
-    // dependency chains instead of one (r06 stamps: the loop is latency-, not issue-bound).
-    // Unquantised P only: -5 % kernel time there, but +9 % with the FP8 P qdq of both tiles live
-    // at once (scripts/exp/bench_attn_exp.py A/B, profiles/r06/attention/ab_interleave_*)
-    const bool both = AHEAD && PQ == 0 && NSUB == 2 && active && kvs + kKv < w_end;
-    if (both) {
-      s_b = score(1);
-      const int kva = kvs, kvb = kvs + kKv;
-      const bool mask_a = kva + kKv > lk || (a.causal && kva + kKv - 1 > q0 + off);
-      const bool mask_b = kvb + kKv > lk || (a.causal && kvb + kKv - 1 > q0 + off);
-      float xa[16], xb[16], pa[16], pb[16];
-      const float mla = xmax32(scale_x(s_a, mask_a, kva, xa));
-      const float mlb = xmax32(scale_x(s_b, mask_b, kvb, xb));
-      const float mna = fmaxf(m, mla), mnb = fmaxf(mna, mlb);
-      const float mua = mna == kNegInf ? 0.f : mna, mub = mnb == kNegInf ? 0.f : mnb;
-      const float lsa = expsum(xa, mua, pa);
-      const float lsb = expsum(xb, mub, pb);
-      const float corra = m == mna ? 1.f : __builtin_amdgcn_exp2f(m - mua);
-      const float corrb = mna == mnb ? 1.f : __builtin_amdgcn_exp2f(mna - mub);
-      l = l * corra + lsa;
-      l = l * corrb + lsb;
-      float sba[2] = {1.f, 1.f}, sbb[2] = {1.f, 1.f};
-      qdq(pa, sba);
-      qdq(pb, sbb);
-      rescale(corra, m != mna);
-      pv(pa, sba, Vb);
-      rescale(corrb, mna != mnb);
-      pv(pb, sbb, Vb + kKv * VPITCH);
-      m = mnb;
-    } else {
+    {
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {
     const int kv0 = kvs + sub * kKv;
