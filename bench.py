@@ -315,8 +315,10 @@ def awq_search_suite(rounds: int = 3):
 
         arms = {"fused_search": fused, "batched_hipblaslt_path": batched, "hipblaslt_gemms_alone": gemms}
         t = {k: [] for k in arms}
-        for _ in range(rounds):
-            for k, f in arms.items():
+        names = list(arms)
+        for r_ in range(rounds):  # the order rotates per round (a fixed order biases an arm by ~4 %)
+            for k in names[r_ % len(names):] + names[:r_ % len(names)]:
+                f = arms[k]
                 f()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

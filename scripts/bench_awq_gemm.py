@@ -78,9 +78,10 @@ for name, (N, K) in SHAPES.items():
 
     arms = {"fused": search, "fused_pp": search_pp, "batched": batched, "per_alpha": per_alpha, "hipblaslt_gemms": hipblaslt_gemms}
     t = {k: [] for k in arms}
-    for _ in range(ROUNDS):
-        for k, f in arms.items():
-            t[k].append(timeit(f))
+    names = list(arms)
+    for r_ in range(ROUNDS):  # rotated order per round: a fixed order biases an arm by ~4 %
+        for k in names[r_ % len(names):] + names[:r_ % len(names)]:
+            t[k].append(timeit(arms[k]))
     flops = 2.0 * M * N * K * G
     r = {}
     for k, v in t.items():
